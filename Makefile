@@ -1,0 +1,33 @@
+# Build recipes (no cmake needed).  `make` builds the product library and the CPU oracle.
+#   dirt_amd/libdirt_mi355x.so  -- HIP kernels + C ABI (include/dirt_mi355x.h), gfx950 only
+#   oracle/libdirt_oracle.so    -- CPU oracle (test infrastructure only)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CC ?= gcc
+
+# -ffp-contract=off + correctly rounded divide: the raster rules are stated as
+# single IEEE operations so that the HIP path and the oracle agree bit-exactly on coverage and depth.
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+           -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function
+ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall
+
+LIB = dirt_amd/libdirt_mi355x.so
+ORACLE = oracle/libdirt_oracle.so
+HIP_SRC = dirt_amd/csrc/dirt_raster.hip
+HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/raster_rules.h include/dirt_mi355x.h
+
+all: $(LIB) $(ORACLE)
+
+$(LIB): $(HIP_DEPS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRC)
+
+$(ORACLE): oracle/dirt_oracle.c
+	$(CC) $(ORACLE_CFLAGS) -shared -o $@ $< -lm
+
+asm: $(HIP_DEPS)
+	mkdir -p build/asm && cd build/asm && $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o dirt_raster.s ../../$(HIP_SRC)
+
+clean:
+	rm -f $(LIB) $(ORACLE)
+
+.PHONY: all clean asm

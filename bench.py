@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Benchmark of the dirt rasterise hot path (forward + backward) on MI355X.
+
+Metric (BASELINE.json): Mpixels/s fwd+bwd at 1024x1024, 50k random triangles (config 3).
+One step = dirt rasterise forward + registered backward over one synthetic frame per rank
+(SURVEY 8d distribution, seed = rank), inputs resident in HBM.  N>1: one process per GPU, frames
+sharded across ranks with no data-path collective (weak scaling); value = all ranks' pixels / max time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  Extra keys: roofline (dominant kernel, HIP-event timed), cpu_baseline
+(the CPU oracle on the box's host cores, rank 0 at N=1), kernels (per-kernel average microseconds).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
+
+CONFIGS = {
+    # name: (B per rank, H, W, C, F, radius_px)
+    "c3": (1, 1024, 1024, 3, 50000, 16.0),
+    "c5": (8, 1024, 1024, 3, 20000, 16.0),  # 64 frames over 8 GPUs -> 8 per rank
+    "c3_r64": (1, 1024, 1024, 3, 50000, 64.0),
+}
+
+
+def alg_bytes(B, H, W, C, V, F):
+    """Algorithmic HBM bytes (tensor I/O of the op) per kernel and per op."""
+    hwc, hw = 4 * C * H * W, 4 * H * W
+    k = {
+        "raster_kernel": B * (2 * hwc + hw + 4 * C * V + 12 * F),
+        "grad_kernel": B * (3 * hwc + hw + 16 * V + 12 * F + 16 * V + 4 * C * V),
+        "setup_kernel": B * (12 * F + 16 * V),
+    }
+    fwd = B * (16 * V + 12 * F + 4 * C * V + 2 * hwc)
+    bwd = B * (16 * V + 12 * F + 4 * C * V + 2 * hwc + 16 * V + 4 * C * V + hwc)
+    return k, fwd, bwd
+
+
+def make_inputs(cfg, rank, device):
+    import scenes
+    B, H, W, C, F, r = cfg
+    frames = [scenes.random_triangles(F=F, W=W, H=H, C=C, radius_px=r, seed=rank * B + b) for b in range(B)]
+    host = [np.stack([fr[k] for fr in frames]) for k in range(4)]
+    dev = [torch.from_numpy(a).to(device) for a in host]
+    g = np.random.default_rng(10_000 + rank).standard_normal(host[0].shape).astype(np.float32)
+    return host, dev, torch.from_numpy(g).to(device), g
+
+
+def cpu_baseline(host, grad_host, budget_s=10.0, max_reps=20):
+    from oracle import oracle
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    bg, v, c, f = host
+    B, H, W, C = bg.shape
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < max_reps and (time.perf_counter() - t_start < budget_s or len(times) < 1):
+        t0 = time.perf_counter()
+        px, gb, _ = oracle.rasterise_fwd(bg, v, c, f, nthreads=nthreads)
+        oracle.rasterise_bwd(v, c, f, px, grad_host, gb, nthreads=nthreads)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": B * H * W / t / 1e6, "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
+            "sample": "%d x full config frame(s) (%dx%dx%d, F=%d) fwd+bwd, median of %d reps, oracle/dirt_oracle.c "
+                      "OpenMP" % (B, H, W, C, f.shape[1], len(times)),
+            "ms_per_frame": t * 1e3 / B}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--profile-steps", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    from dirt_amd import _lib
+    from dirt_amd.session import RasteriseSession
+
+    cfg = CONFIGS[args.config]
+    B, H, W, C, F, _r = cfg
+    V = 3 * F
+    host, (bg, v, c, f), grad, grad_host = make_inputs(cfg, rank, device)
+    sess = RasteriseSession(B, H, W, C, V, F, device=device)
+
+    def step():
+        sess.forward(bg, v, c, f)
+        sess.backward(grad)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    run = step
+    if not args.no_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        for _ in range(3):
+            graph.replay()
+        run = graph.replay
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * B * H * W * args.steps / elapsed / 1e6
+
+    # per-kernel HIP-event timing (same kernels, eager launches, outside the timed loop)
+    _lib.profile_enable(True)
+    for _ in range(args.profile_steps):
+        step()
+    torch.cuda.synchronize()
+    prof = _lib.profile_read()
+    _lib.profile_enable(False)
+    kern_us = {k: (ms / n * 1e3 if n else 0.0) for k, (n, ms) in prof.items()}
+    kbytes, fwd_b, bwd_b = alg_bytes(B, H, W, C, V, F)
+    dom = max((k for k in kern_us if k in kbytes), key=lambda k: kern_us[k])
+    achieved = kbytes[dom] / (kern_us[dom] * 1e-6) / 1e9
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_launch": kbytes[dom], "avg_us": round(kern_us[dom], 2),
+                "op_frac": round((fwd_b + bwd_b) / (ms_per_step * 1e-3 / world) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(host, grad_host, budget_s=args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": "Mpixels/s fwd+bwd @1024^2 50k-tri",
+            "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "%s: %d frame(s)/rank x %d random tris (r=%gpx), %dx%dx%d, fwd+bwd" %
+                                   (args.config, B, F, _r, H, W, C),
+                       "frames_per_rank": B, "height": H, "width": W, "channels": C, "faces": F, "vertices": V,
+                       "parallelism": "frames sharded over %d rank(s), no collective in step" % world,
+                       "hip_graph": not args.no_graph},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels_us": {k: round(u, 2) for k, u in kern_us.items()},
+        }
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

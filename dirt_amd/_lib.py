@@ -1,0 +1,101 @@
+"""ctypes binding of libdirt_mi355x.so (the C ABI in include/dirt_mi355x.h).
+
+This is the Python analogue of `tf.load_op_library(_lib_path + '/librasterise.so')`
+(reference dirt/rasterise_ops.py:6-7): the shared library is loaded from the package directory.
+There is no fallback: if the library is missing or cannot be loaded the import of the op fails loudly.
+"""
+import ctypes
+import os
+
+_here = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DIRT_MI355X_LIB", os.path.join(_here, "libdirt_mi355x.so"))
+
+DIRT_OK = 0
+DIRT_EINVAL = 1
+DIRT_EFACE = 2
+DIRT_EHIP = 3
+
+SHADER_GOURAUD = 0
+SHADER_OCEANIC_HORIZON = 1
+
+MAX_CHANNELS = 8
+MAX_DIM = 8192
+
+# every symbol include/dirt_mi355x.h declares, with its ctypes signature
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_SZ = ctypes.c_size_t
+SIGNATURES = {
+    "dirt_abi_version": (_I, []),
+    "dirt_workspace_sizes": (_I, [_I, _I, _I, _I, _I, _I, _I64, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "dirt_rasterise_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _P]),
+    "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
+    "dirt_profile_enable": (_I, [_I]),
+    "dirt_profile_read": (_I, [_I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double)]),
+    "dirt_last_error": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class DirtError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the library, raising if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libdirt_mi355x.so not found at %s; build it with `make` (or __graft_entry__.build())" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    """Map a C-ABI return code to a Python exception (mirrors OP_REQUIRES -> InvalidArgument)."""
+    if rc == DIRT_OK:
+        return
+    msg = load().dirt_last_error().decode("utf-8", "replace")
+    if rc == DIRT_EINVAL:
+        raise ValueError(msg)
+    if rc == DIRT_EFACE:
+        raise IndexError(msg)
+    raise DirtError(msg)
+
+
+def workspace_sizes(B, H, W, C, V, F, bin_capacity=0):
+    lib = load()
+    saved = ctypes.c_size_t(0)
+    scratch = ctypes.c_size_t(0)
+    check(lib.dirt_workspace_sizes(B, H, W, C, V, F, bin_capacity, ctypes.byref(saved), ctypes.byref(scratch)))
+    return saved.value, scratch.value
+
+
+NUM_KERNELS = 5
+
+
+def profile_enable(on=True):
+    check(load().dirt_profile_enable(1 if on else 0))
+
+
+def profile_read():
+    """{kernel name: (launches, total_ms)} for the launches recorded since profile_enable(True)."""
+    lib = load()
+    out = {}
+    for k in range(NUM_KERNELS):
+        name = ctypes.c_char_p()
+        n = ctypes.c_int(0)
+        ms = ctypes.c_double(0)
+        check(lib.dirt_profile_read(k, ctypes.byref(name), ctypes.byref(n), ctypes.byref(ms)))
+        out[name.value.decode()] = (n.value, ms.value)
+    return out

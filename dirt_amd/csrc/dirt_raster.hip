@@ -1,0 +1,736 @@
+// dirt_raster.hip -- MI355X (gfx950) software rasteriser behind the C ABI of include/dirt_mi355x.h.
+//
+// CDNA4 has no graphics pipeline, so the reference's GL fixed-function raster
+// (csrc/rasterise_egl.cpp:440-487 + the NVIDIA driver) becomes a compute pipeline:
+//
+//   K1 setup_kernel    one thread per (frame, face): fetch 3 clip vertices, project + snap (R1/R2),
+//                      edge equations (R3), depth plane (R4), guard-band clipping (R5, rare slow path);
+//                      writes 128-B setup records and counts (tile, triangle) bin entries.
+//   K2 scan_kernel     exclusive scan of per-tile counts.
+//   K3 fill_kernel     scatter each record index into the bins of the 16x16 tiles its bbox overlaps.
+//   K4 raster_kernel   one 256-thread workgroup per 16x16 tile: stages the tile's records in LDS,
+//                      each lane owns one pixel and keeps the min (depth24<<32 | face) key, then
+//                      resolves in-kernel: perspective-correct Gouraud colour (R6) or background,
+//                      coalesced [B,H,W,C] writes + the int32 g-buffer.  This fuses the reference's
+//                      upload_background + raster + second pass + download_pixels
+//                      (csrc/rasterise_egl.cu:16-129, rasterise_egl.cpp:370-503) into one pass over HBM.
+//   K5 grad_kernel     backward: dL/dbackground, dL/dvertex_colors and the
+//                      filter-based dL/dvertices (README.md:146-147) for the gradient contract of
+//                      csrc/rasterise_grad_common.h:19-24.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/dirt_mi355x.h"
+#include "raster_rules.h"
+
+using namespace dirt;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+// ------------------------------------------------------------------------------------------------
+// Optional per-kernel event timing (bench.py roofline); off by default, host-side only.
+enum KernelId { K_SETUP = 0, K_SCAN, K_FILL, K_RASTER, K_GRAD, K_COUNT };
+const char *const kKernelNames[K_COUNT] = {"setup_kernel", "scan_kernel", "fill_kernel", "raster_kernel",
+                                           "grad_kernel"};
+struct Profiler {
+    bool enabled = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[K_COUNT];
+} g_prof;
+
+struct ProfScope {
+    hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t s;
+    int id;
+    ProfScope(int id_, hipStream_t s_) : s(s_), id(id_)
+    {
+        if (!g_prof.enabled) return;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
+        (void)hipEventRecord(a, s);
+    }
+    ~ProfScope()
+    {
+        if (!a) return;
+        (void)hipEventRecord(b, s);
+        g_prof.ev[id].emplace_back(a, b);
+    }
+};
+
+int fail(int code, const char *msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess) {                                                         \
+            char _b[256];                                                               \
+            snprintf(_b, sizeof(_b), "%s failed: %s", #expr, hipGetErrorString(_e));    \
+            return fail(DIRT_EHIP, _b);                                                 \
+        }                                                                               \
+    } while (0)
+
+inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// ------------------------------------------------------------------------------------------------
+// Workspace layout
+struct Layout {
+    int ntx, nty, ntiles;       // tiles per frame
+    int64_t nrec;               // records per frame = 6F
+    size_t saved_recs, saved_nsub, saved_total;
+    size_t off_count, off_cursor, off_offset, off_scan_tmp, off_flag, off_bins, scratch_total;
+    size_t scan_tmp_bytes;
+    int64_t bin_capacity;
+};
+
+int64_t default_capacity(int B, int F, int ntiles)
+{
+    int64_t c = 16 * (int64_t)B * (int64_t)F + 4 * (int64_t)B * ntiles;
+    if (c < (1 << 20)) c = 1 << 20;
+    if (c > 0x7fffffffLL) c = 0x7fffffffLL;
+    return c;
+}
+
+int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
+{
+    L.ntx = (W + kTile - 1) / kTile;
+    L.nty = (H + kTile - 1) / kTile;
+    L.ntiles = L.ntx * L.nty;
+    L.nrec = (int64_t)(1 + kExtraPerFace) * F;
+    L.bin_capacity = bin_capacity > 0 ? (bin_capacity > 0x7fffffffLL ? 0x7fffffffLL : bin_capacity)
+                                      : default_capacity(B, F, L.ntiles);
+    L.saved_recs = 0;
+    L.saved_nsub = (size_t)align_up((int64_t)B * L.nrec * (int64_t)sizeof(Rec), 256);
+    L.saved_total = L.saved_nsub + (size_t)align_up((int64_t)B * F * 4, 256);
+    const int64_t nt = (int64_t)B * L.ntiles;
+    const size_t tmp = 0;
+    L.scan_tmp_bytes = tmp;
+    size_t o = 0;
+    L.off_count = o;  o += (size_t)align_up(nt * 4, 256);
+    L.off_cursor = o; o += (size_t)align_up(nt * 4, 256);
+    L.off_offset = o; o += (size_t)align_up(nt * 8, 256);
+    L.off_flag = o;   o += 256;
+    L.off_scan_tmp = o; o += (size_t)align_up((int64_t)tmp, 256);
+    L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 4, 256);
+    L.scratch_total = o;
+    return DIRT_OK;
+}
+
+int validate(int B, int H, int W, int C, int V, int F)
+{
+    if (B < 0 || V < 0 || F < 0) return fail(DIRT_EINVAL, "Rasterise expects non-negative batch, vertex and face counts");
+    if (H <= 0 || W <= 0 || H > DIRT_MAX_DIM || W > DIRT_MAX_DIM)
+        return fail(DIRT_EINVAL, "Rasterise expects 0 < height, width <= 8192");
+    if (C < 1 || C > DIRT_MAX_CHANNELS) return fail(DIRT_EINVAL, "Rasterise expects 1 <= channels <= 8");
+    if ((int64_t)B * F > 0x0fffffffLL || (int64_t)B * V > 0x7fffffffLL)
+        return fail(DIRT_EINVAL, "Rasterise batch too large");
+    return DIRT_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1: setup
+
+__device__ inline bool finite4(const float *v)
+{
+    return __builtin_isfinite(v[0]) && __builtin_isfinite(v[1]) && __builtin_isfinite(v[2]) && __builtin_isfinite(v[3]);
+}
+
+__device__ inline float plane_dist(int p, const float *v, float gx, float gy)
+{
+    switch (p) {
+    case 0: return v[2] + v[3];
+    case 1: return gx * v[3] + v[0];
+    case 2: return gx * v[3] - v[0];
+    case 3: return gy * v[3] + v[1];
+    default: return gy * v[3] - v[1];
+    }
+}
+
+// R5 slow path: clip against z>=-w and the guard planes, fan-triangulate. Returns nsub.
+__device__ __noinline__ int clip_face(const float (*v)[4], int W, int H, int F, int f, Rec *frame_recs)
+{
+    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+    float poly[9][7], tmp[9][7];
+    int n = 3;
+    for (int k = 0; k < 3; ++k) {
+        for (int c = 0; c < 4; ++c) poly[k][c] = v[k][c];
+        for (int i = 0; i < 3; ++i) poly[k][4 + i] = (i == k) ? 1.0f : 0.0f;
+    }
+    for (int p = 0; p < 5; ++p) {
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const float *a = poly[i];
+            const float *c = poly[(i + 1) % n];
+            const float da = plane_dist(p, a, gx, gy), dc = plane_dist(p, c, gx, gy);
+            const bool ina = da >= 0.0f, inc = dc >= 0.0f;
+            if (ina) {
+                for (int q = 0; q < 7; ++q) tmp[m][q] = a[q];
+                ++m;
+            }
+            if (ina != inc) {
+                const float t = da / (da - dc);
+                for (int q = 0; q < 7; ++q) tmp[m][q] = a[q] + t * (c[q] - a[q]);
+                ++m;
+            }
+        }
+        n = m;
+        if (n < 3) return 0;
+        for (int i = 0; i < n; ++i)
+            for (int q = 0; q < 7; ++q) poly[i][q] = tmp[i][q];
+    }
+    for (int i = 0; i < n; ++i)
+        if (!(poly[i][3] > 0.0f)) return 0;
+    const int nsub = n - 2;
+    for (int s = 0; s < nsub; ++s) {
+        float sv[3][4], sb[3][3];
+        const int idx[3] = {0, s + 1, s + 2};
+        for (int k = 0; k < 3; ++k) {
+            for (int c = 0; c < 4; ++c) sv[k][c] = poly[idx[k]][c];
+            for (int i = 0; i < 3; ++i) sb[k][i] = poly[idx[k]][4 + i];
+        }
+        make_record(sv, sb, W, H, f, &frame_recs[rec_index(F, f, s)]);
+    }
+    return nsub;
+}
+
+__device__ inline void count_tiles(const Rec &r, int ntx, uint32_t *tile_count_frame)
+{
+    if (r.i0 > r.i1) return;
+    const int tx0 = r.i0 / kTile, tx1 = r.i1 / kTile, ty0 = r.j0 / kTile, ty1 = r.j1 / kTile;
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&tile_count_frame[ty * ntx + tx], 1u);
+}
+
+__global__ __launch_bounds__(256) void setup_kernel(const float *__restrict__ verts, const int32_t *__restrict__ faces,
+                                                    int B, int V, int F, int W, int H, int ntx, int ntiles, int64_t nrec,
+                                                    Rec *__restrict__ recs, int32_t *__restrict__ nsub,
+                                                    uint32_t *__restrict__ tile_count, uint32_t *__restrict__ flag)
+{
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (int64_t)B * F) return;
+    const int b = (int)(gid / F), f = (int)(gid - (int64_t)b * F);
+    Rec *frame_recs = recs + (int64_t)b * nrec;
+    const int32_t *f3 = faces + gid * 3;
+    const float *vb = verts + (int64_t)b * V * 4;
+    float v[3][4];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int32_t vi = f3[k];
+        if (vi < 0 || vi >= V) {
+            ok = false;
+            atomicOr(flag, 1u);
+            v[k][0] = v[k][1] = v[k][2] = 0.0f; v[k][3] = 1.0f;
+        } else {
+            const float4 p = *reinterpret_cast<const float4 *>(vb + (int64_t)vi * 4);
+            v[k][0] = p.x; v[k][1] = p.y; v[k][2] = p.z; v[k][3] = p.w;
+            ok = ok && finite4(v[k]);
+        }
+    }
+    uint32_t *tc = tile_count + (int64_t)b * ntiles;
+    Rec &r0 = frame_recs[f];
+    if (!ok) {
+        set_empty(&r0, f);
+        nsub[gid] = 0;
+        return;
+    }
+    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+    bool fast = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float w = v[k][3];
+        fast = fast && (w > 0.0f && fabsf(v[k][0]) <= gx * w && fabsf(v[k][1]) <= gy * w);
+    }
+    if (fast) {
+        const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
+        Rec r;
+        make_record(v, id, W, H, f, &r);
+        r0 = r;
+        nsub[gid] = 1;
+        count_tiles(r, ntx, tc);
+        return;
+    }
+    set_empty(&r0, f);
+    const int n = clip_face(v, W, H, F, f, frame_recs);
+    nsub[gid] = n;
+    for (int s = 0; s < n; ++s) count_tiles(frame_recs[rec_index(F, f, s)], ntx, tc);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2: exclusive scan of the per-tile counts (one workgroup; B*ntiles is 4096 per 1024^2 frame)
+
+constexpr int kScanThreads = 1024;
+constexpr int kScanPerThread = 4;
+
+__global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                            int64_t n)
+{
+    __shared__ uint64_t wave_sums[kScanThreads / 64];
+    __shared__ uint64_t carry_s;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint64_t carry = 0;
+    for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kScanPerThread) {
+        const int64_t k0 = base + (int64_t)t * kScanPerThread;
+        uint32_t v[kScanPerThread];
+        uint64_t local = 0;
+#pragma unroll
+        for (int q = 0; q < kScanPerThread; ++q) {
+            v[q] = (k0 + q < n) ? in[k0 + q] : 0u;
+            local += v[q];
+        }
+        // inclusive wave scan of the per-thread sums
+        uint64_t x = local;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wave_sums[wave] = x;
+        __syncthreads();
+        if (wave == 0) {
+            uint64_t w = lane < kScanThreads / 64 ? wave_sums[lane] : 0;
+#pragma unroll
+            for (int d = 1; d < kScanThreads / 64; d <<= 1) {
+                const uint64_t y = __shfl_up(w, d, 64);
+                if (lane >= d) w += y;
+            }
+            if (lane < kScanThreads / 64) wave_sums[lane] = w;  // inclusive
+            if (lane == kScanThreads / 64 - 1) carry_s = w;
+        }
+        __syncthreads();
+        uint64_t run = carry + (wave > 0 ? wave_sums[wave - 1] : 0) + (x - local);
+#pragma unroll
+        for (int q = 0; q < kScanPerThread; ++q) {
+            if (k0 + q < n) out[k0 + q] = run;
+            run += v[q];
+        }
+        carry += carry_s;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K3: fill bins (order inside a bin is irrelevant: the depth resolve is a commutative min)
+
+__global__ __launch_bounds__(256) void fill_kernel(const Rec *__restrict__ recs, const int32_t *__restrict__ nsub,
+                                                   int B, int F, int ntx, int ntiles, int64_t nrec,
+                                                   const uint64_t *__restrict__ tile_offset,
+                                                   uint32_t *__restrict__ tile_cursor, int32_t *__restrict__ bins,
+                                                   int64_t capacity)
+{
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (int64_t)B * F) return;
+    const int b = (int)(gid / F), f = (int)(gid - (int64_t)b * F);
+    const int n = nsub[gid];
+    for (int s = 0; s < n; ++s) {
+        const int64_t ri = rec_index(F, f, s);
+        const Rec &r = recs[(int64_t)b * nrec + ri];
+        if (r.i0 > r.i1) continue;
+        const int tx0 = r.i0 / kTile, tx1 = r.i1 / kTile, ty0 = r.j0 / kTile, ty1 = r.j1 / kTile;
+        for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+                const int64_t t = (int64_t)b * ntiles + ty * ntx + tx;
+                const uint32_t pos = atomicAdd(&tile_cursor[t], 1u);
+                const uint64_t dst = tile_offset[t] + pos;
+                if (dst < (uint64_t)capacity) bins[dst] = (int32_t)ri;
+            }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K4: tile raster + resolve
+
+struct PixelState {
+    uint64_t best;
+    int32_t best_rec;
+};
+
+__device__ __forceinline__ void raster_one(const RasterPart &R, int32_t ri, int i, int j, PixelState &st)
+{
+    int64_t E[3];
+    edge_values(R, i, j, E);
+    if (!inside(R, E)) return;
+    uint32_t d;
+    if (!sample_depth(R, i, j, d)) return;
+    const uint64_t key = ((uint64_t)d << 32) | (uint32_t)R.face;
+    if (key < st.best) {
+        st.best = key;
+        st.best_rec = ri;
+    }
+}
+
+template <int CC>
+__global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
+                                                     const int32_t *__restrict__ faces, const Rec *__restrict__ recs,
+                                                     const int32_t *__restrict__ nsub,
+                                                     const uint32_t *__restrict__ tile_count,
+                                                     const uint64_t *__restrict__ tile_offset,
+                                                     const int32_t *__restrict__ bins, int64_t capacity,
+                                                     int B, int H, int W, int Cdyn, int V, int F, int ntx, int ntiles,
+                                                     int64_t nrec, float *__restrict__ pixels, int32_t *__restrict__ gbuffer)
+{
+    const int C = CC > 0 ? CC : Cdyn;
+    __shared__ RasterPart lds_rec[256];
+    __shared__ int32_t lds_idx[256];
+    const int tile = blockIdx.x, b = blockIdx.y;
+    const int tx = tile % ntx, ty = tile / ntx;
+    const int t = threadIdx.x, lx = t & 15, ly = t >> 4, wave = t >> 6;
+    const int i = tx * kTile + lx, j = ty * kTile + ly;
+    const int sx0 = tx * kTile, sx1 = sx0 + kTile - 1, sy0 = ty * kTile + wave * 4, sy1 = sy0 + 3;
+    const Rec *frame_recs = recs + (int64_t)b * nrec;
+    PixelState st{~0ull, -1};
+
+    const int64_t tt = (int64_t)b * ntiles + tile;
+    const uint32_t cnt = tile_count[tt];
+    const uint64_t off = tile_offset[tt];
+    if (off + cnt <= (uint64_t)capacity) {
+        for (uint32_t base = 0; base < cnt; base += 256) {
+            const int n = (int)min(256u, cnt - base);
+            __syncthreads();
+            if (t < n) {
+                const int32_t ri = bins[off + base + t];
+                const uint4 *src = reinterpret_cast<const uint4 *>(frame_recs + ri);
+                uint4 *dst = reinterpret_cast<uint4 *>(&lds_rec[t]);
+#pragma unroll
+                for (int q = 0; q < 5; ++q) dst[q] = src[q];
+                lds_idx[t] = ri;
+            }
+            __syncthreads();
+            for (int e = 0; e < n; ++e) {
+                const RasterPart &R = lds_rec[e];
+                const int bi0 = __builtin_amdgcn_readfirstlane(R.i0), bi1 = __builtin_amdgcn_readfirstlane(R.i1);
+                const int bj0 = __builtin_amdgcn_readfirstlane(R.j0), bj1 = __builtin_amdgcn_readfirstlane(R.j1);
+                if (bi1 < sx0 || bi0 > sx1 || bj1 < sy0 || bj0 > sy1) continue;
+                raster_one(R, lds_idx[e], i, j, st);
+            }
+        }
+    } else {
+        // bin overflow (capacity too small for this input): scan every record of the frame
+        for (int f = 0; f < F; ++f) {
+            const int n = nsub[(int64_t)b * F + f];
+            for (int s = 0; s < n; ++s) {
+                const int64_t ri = rec_index(F, f, s);
+                const Rec &r = frame_recs[ri];
+                if (r.i0 > r.i1 || r.i1 < sx0 || r.i0 > sx1 || r.j1 < sy0 || r.j0 > sy1) continue;
+                RasterPart R;
+                memcpy(&R, &r, sizeof(RasterPart));
+                raster_one(R, (int32_t)ri, i, j, st);
+            }
+        }
+    }
+
+    if (i >= W || j >= H) return;
+    const int row = H - 1 - j;
+    const int64_t o = ((int64_t)b * H + row) * W + i;
+    gbuffer[o] = st.best_rec;
+    float *out = pixels + o * C;
+    if (st.best_rec < 0) {
+        const float *bg = background + o * C;
+        for (int c = 0; c < C; ++c) out[c] = bg[c];
+        return;
+    }
+    const Rec r = frame_recs[st.best_rec];
+    int64_t E[3];
+    edge_values(r, i, j, E);
+    float lam[3] = {0.0f, 0.0f, 0.0f};
+    parent_lambda(r, E, lam);
+    const int32_t *f3 = faces + ((int64_t)b * F + r.face) * 3;
+    const float *cb = colors + (int64_t)b * V * C;
+    const float *c0 = cb + (int64_t)f3[0] * C, *c1 = cb + (int64_t)f3[1] * C, *c2 = cb + (int64_t)f3[2] * C;
+    for (int c = 0; c < C; ++c) out[c] = (lam[0] * c0[c] + lam[1] * c1[c]) + lam[2] * c2[c];
+}
+
+// ------------------------------------------------------------------------------------------------
+// K5: backward (first version: per-pixel contributions, global float atomics)
+
+__device__ bool covers_face(const Rec *frame_recs, const int32_t *nsub_frame, int F, int f, int i, int j)
+{
+    const int n = nsub_frame[f];
+    for (int s = 0; s < n; ++s) {
+        const Rec &r = frame_recs[rec_index(F, f, s)];
+        if (r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1) continue;
+        int64_t E[3];
+        edge_values(r, i, j, E);
+        if (inside(r, E)) return true;
+    }
+    return false;
+}
+
+__device__ void add_pair_owner(const Rec &r, const float *vb, const int32_t *fb, int W, int H, int i, int j, int i2,
+                               int j2, int axis, float s, float omega, float *gvb)
+{
+    int64_t E1[3], E2[3], E[3];
+    edge_values(r, i, j, E1);
+    edge_values(r, i2, j2, E2);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E[k] = E1[k] + E2[k];
+    float lam[3];
+    if (!parent_lambda(r, E, lam)) return;
+    const int32_t *f3 = fb + 3 * (int64_t)r.face;
+    const float w0 = vb[(int64_t)f3[0] * 4 + 3], w1 = vb[(int64_t)f3[1] * 4 + 3], w2 = vb[(int64_t)f3[2] * 4 + 3];
+    const float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
+    if (Wm == 0.0f) return;
+    const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
+    const float mid = axis == 0 ? (float)(i + 1) : (float)(j + 1);
+    const float ndc = mid / half - 1.0f;
+    const float tt = ((omega * s) * half) / Wm;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float g = tt * lam[k];
+        float *d = gvb + (int64_t)f3[k] * 4;
+        atomicAdd(d + axis, g);
+        atomicAdd(d + 3, -(g * ndc));
+    }
+}
+
+__global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ verts, const int32_t *__restrict__ faces,
+                                                   const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+                                                   const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
+                                                   const int32_t *__restrict__ nsub, int B, int H, int W, int C, int V,
+                                                   int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
+                                                   float *__restrict__ grad_colors, float *__restrict__ grad_bg)
+{
+    const int tile = blockIdx.x, b = blockIdx.y;
+    const int tx = tile % ntx, ty = tile / ntx;
+    const int t = threadIdx.x;
+    const int i = tx * kTile + (t & 15), j = ty * kTile + (t >> 4);
+    if (i >= W || j >= H) return;
+    const Rec *frame_recs = recs + (int64_t)b * nrec;
+    const int32_t *nsub_frame = nsub + (int64_t)b * F;
+    const float *vb = verts + (int64_t)b * V * 4;
+    const int32_t *fb = faces + (int64_t)b * F * 3;
+    float *gvb = grad_verts + (int64_t)b * V * 4;
+    float *gcb = grad_colors + (int64_t)b * V * C;
+    const int row = H - 1 - j;
+    const int64_t o = ((int64_t)b * H + row) * W + i;
+    const float *G = grad_pixels + o * C, *I = pixels + o * C;
+    const int32_t rp = gbuffer[o];
+    float *gbg = grad_bg + o * C;
+    if (rp < 0) {
+        for (int c = 0; c < C; ++c) gbg[c] = G[c];
+    } else {
+        for (int c = 0; c < C; ++c) gbg[c] = 0.0f;
+        const Rec &r = frame_recs[rp];
+        int64_t E[3];
+        edge_values(r, i, j, E);
+        float lam[3];
+        if (parent_lambda(r, E, lam)) {
+            const int32_t *f3 = fb + 3 * (int64_t)r.face;
+            for (int k = 0; k < 3; ++k)
+                for (int c = 0; c < C; ++c) atomicAdd(gcb + (int64_t)f3[k] * C + c, lam[k] * G[c]);
+        }
+    }
+    for (int axis = 0; axis < 2; ++axis) {
+        const int i2 = i + (axis == 0), j2 = j + (axis == 1);
+        if (i2 >= W || j2 >= H) continue;
+        const int64_t o2 = ((int64_t)b * H + (H - 1 - j2)) * W + i2;
+        const int32_t rq = gbuffer[o2];
+        if (rp < 0 && rq < 0) continue;
+        const float *G2 = grad_pixels + o2 * C, *I2 = pixels + o2 * C;
+        float acc = 0.0f;
+        for (int c = 0; c < C; ++c) acc += (G[c] + G2[c]) * (I2[c] - I[c]);
+        const float s = -0.5f * acc;
+        if (s == 0.0f) continue;
+        const int fp = rp >= 0 ? frame_recs[rp].face : -1, fq = rq >= 0 ? frame_recs[rq].face : -1;
+        if (fp == fq || fq < 0) {
+            add_pair_owner(frame_recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
+        } else if (fp < 0) {
+            add_pair_owner(frame_recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
+        } else {
+            const bool cfq = covers_face(frame_recs, nsub_frame, F, fp, i2, j2);
+            const bool cgp = covers_face(frame_recs, nsub_frame, F, fq, i, j);
+            if (!cfq && cgp) {
+                add_pair_owner(frame_recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
+            } else if (cfq && !cgp) {
+                add_pair_owner(frame_recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
+            } else {
+                add_pair_owner(frame_recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gvb);
+                add_pair_owner(frame_recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gvb);
+            }
+        }
+    }
+}
+
+__global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n, int V, uint32_t *flag)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        if (faces[k] < 0 || faces[k] >= V) atomicOr(flag, 1u);
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+
+extern "C" {
+
+int dirt_abi_version(void) { return 1; }
+
+const char *dirt_last_error(void) { return g_last_error.c_str(); }
+
+int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_capacity, size_t *saved_bytes,
+                         size_t *scratch_bytes)
+{
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    Layout L;
+    rc = make_layout(B, H, W, F, bin_capacity, L);
+    if (rc) return rc;
+    if (saved_bytes) *saved_bytes = L.saved_total;
+    if (scratch_bytes) *scratch_bytes = L.scratch_total;
+    return DIRT_OK;
+}
+
+int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
+                       const int32_t *faces, const float *camera_pos, int B, int H, int W, int C, int V, int F,
+                       int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch,
+                       size_t scratch_bytes, int64_t bin_capacity, void *stream_)
+{
+    (void)camera_pos;
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    if (shader_id != DIRT_SHADER_GOURAUD) return fail(DIRT_EINVAL, "Rasterise: unsupported shader_id");
+    if (B == 0) return DIRT_OK;
+    if (!background || !pixels || !gbuffer || !saved || !scratch || (F > 0 && (!faces || !vertices)) ||
+        (V > 0 && (!vertices || !vertex_colors)))
+        return fail(DIRT_EINVAL, "Rasterise: null tensor pointer");
+    Layout L;
+    rc = make_layout(B, H, W, F, bin_capacity, L);
+    if (rc) return rc;
+    if (saved_bytes < L.saved_total || scratch_bytes < L.scratch_total)
+        return fail(DIRT_EINVAL, "Rasterise: workspace smaller than dirt_workspace_sizes()");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    char *sv = static_cast<char *>(saved), *sc = static_cast<char *>(scratch);
+    Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
+    int32_t *nsub = reinterpret_cast<int32_t *>(sv + L.saved_nsub);
+    uint32_t *tile_count = reinterpret_cast<uint32_t *>(sc + L.off_count);
+    uint32_t *tile_cursor = reinterpret_cast<uint32_t *>(sc + L.off_cursor);
+    uint64_t *tile_offset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
+    int32_t *bins = reinterpret_cast<int32_t *>(sc + L.off_bins);
+    const int64_t nt = (int64_t)B * L.ntiles;
+
+    // counts and cursors are adjacent: one memset (the flag word is left to dirt_check_faces)
+    HIP_TRY(hipMemsetAsync(tile_count, 0, L.off_offset - L.off_count, stream));
+    const int64_t nf = (int64_t)B * F;
+    if (nf > 0) {
+        ProfScope ps(K_SETUP, stream);
+        setup_kernel<<<dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream>>>(
+            vertices, faces, B, V, F, W, H, L.ntx, L.ntiles, L.nrec, recs, nsub, tile_count, flag);
+        HIP_TRY(hipGetLastError());
+    }
+    {
+        ProfScope ps(K_SCAN, stream);
+        scan_kernel<<<dim3(1), dim3(kScanThreads), 0, stream>>>(tile_count, tile_offset, nt);
+    }
+    HIP_TRY(hipGetLastError());
+    if (nf > 0) {
+        ProfScope ps(K_FILL, stream);
+        fill_kernel<<<dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream>>>(
+            recs, nsub, B, F, L.ntx, L.ntiles, L.nrec, tile_offset, tile_cursor, bins, L.bin_capacity);
+        HIP_TRY(hipGetLastError());
+    }
+    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+    ProfScope ps(K_RASTER, stream);
+#define LAUNCH_RASTER(CC)                                                                                       \
+    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, faces, recs, nsub, tile_count,  \
+                                                      tile_offset, bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, \
+                                                      L.ntiles, L.nrec, pixels, gbuffer)
+    if (C == 1) LAUNCH_RASTER(1);
+    else if (C == 3) LAUNCH_RASTER(3);
+    else LAUNCH_RASTER(0);
+#undef LAUNCH_RASTER
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces, const float *pixels,
+                       const float *grad_pixels, const int32_t *gbuffer, const void *saved, int B, int H, int W, int C,
+                       int V, int F, float *grad_vertices, float *grad_vertex_colors, float *grad_background,
+                       void *stream_)
+{
+    (void)vertex_colors;
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    if (B == 0) return DIRT_OK;
+    if (!pixels || !grad_pixels || !gbuffer || !saved || !grad_background || (V > 0 && (!grad_vertices || !grad_vertex_colors || !vertices)) ||
+        (F > 0 && !faces))
+        return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const char *sv = static_cast<const char *>(saved);
+    const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
+    const int32_t *nsub = reinterpret_cast<const int32_t *>(sv + L.saved_nsub);
+    if (V > 0) {
+        HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)B * V * 4 * sizeof(float), stream));
+        HIP_TRY(hipMemsetAsync(grad_vertex_colors, 0, (size_t)B * V * C * sizeof(float), stream));
+    }
+    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+    ProfScope ps(K_GRAD, stream);
+    grad_kernel<<<grid, dim3(256), 0, stream>>>(vertices, faces, pixels, grad_pixels, gbuffer, recs, nsub, B, H, W, C,
+                                                V, F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,
+                                                grad_background);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_profile_enable(int enable)
+{
+    for (int k = 0; k < K_COUNT; ++k) {
+        for (auto &p : g_prof.ev[k]) {
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+        g_prof.ev[k].clear();
+    }
+    g_prof.enabled = enable != 0;
+    return DIRT_OK;
+}
+
+int dirt_profile_read(int kernel_id, const char **name, int *launches, double *total_ms)
+{
+    if (kernel_id < 0 || kernel_id >= K_COUNT) return fail(DIRT_EINVAL, "dirt_profile_read: bad kernel id");
+    double tot = 0.0;
+    for (auto &p : g_prof.ev[kernel_id]) {
+        HIP_TRY(hipEventSynchronize(p.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.first, p.second));
+        tot += ms;
+    }
+    if (name) *name = kKernelNames[kernel_id];
+    if (launches) *launches = (int)g_prof.ev[kernel_id].size();
+    if (total_ms) *total_ms = tot;
+    return DIRT_OK;
+}
+
+int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, size_t scratch_bytes, void *stream_)
+{
+    if (B < 0 || F < 0 || V < 0) return fail(DIRT_EINVAL, "dirt_check_faces: negative size");
+    if (!scratch || scratch_bytes < 512) return fail(DIRT_EINVAL, "dirt_check_faces: scratch too small");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(static_cast<char *>(scratch) + 256 * 0);
+    HIP_TRY(hipMemsetAsync(flag, 0, 4, stream));
+    const int64_t n = (int64_t)B * F * 3;
+    if (n > 0) {
+        check_faces_kernel<<<dim3(1024), dim3(256), 0, stream>>>(faces, n, V, flag);
+        HIP_TRY(hipGetLastError());
+    }
+    uint32_t h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (h) return fail(DIRT_EFACE, "Rasterise: face index out of range [0, vertex count)");
+    return DIRT_OK;
+}
+
+}  // extern "C"

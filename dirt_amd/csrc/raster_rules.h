@@ -1,0 +1,164 @@
+// raster_rules.h -- device-side raster rules R1..R6 of DESIGN.md section 3 (gfx950).
+//
+// These functions are the GPU statement of the rules the CPU oracle (oracle/dirt_oracle.c) states
+// independently.  Both are compiled with -ffp-contract=off and IEEE-correct division so that
+// coverage, 24-bit depth and the visible face are bit-identical; see DESIGN.md section 3.
+//
+// Reference semantics restated: csrc/shaders.cpp:16-34 (clip-space passthrough vertex stage),
+// csrc/rasterise_egl.cpp:194,248,449 (depth test LESS, DEPTH24 cleared to 1.0), :440-458 (faces drawn
+// in index order with base vertex b*V), README.md:134-137 (Gouraud = perspective-correct interpolation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dirt {
+
+constexpr int kTile = 16;          // raster tile edge (pixels); one 256-thread workgroup per tile
+constexpr int kMaxSub = 6;         // fan triangles of a triangle clipped by 5 planes
+constexpr int kExtraPerFace = 5;   // record slots F + 5f + (s-1) for sub-triangles s>0
+constexpr uint32_t kDepthMax = 16777215u;  // 2^24-1 == cleared depth 1.0 (rasterise_egl.cpp:449)
+
+// Per (sub-)triangle setup record, 128 B.  The first 80 B are what the tile raster stages in LDS.
+struct alignas(16) Rec {
+    int32_t A[3];
+    int32_t B[3];
+    int64_t C[3];
+    uint16_t i0, i1, j0, j1;  // inclusive pixel bbox (window coords, j from the bottom); empty if i0 > i1
+    int32_t face;
+    float fx0, fy0, z0, za, zb;  // depth plane relative to snapped vertex 0 (R4)
+    float iw[3];                 // 1/w of the three (sub-)vertices
+    float basis[9];              // row k = parent barycentric of sub-vertex k (identity on the fast path)
+};
+static_assert(sizeof(Rec) == 128, "Rec must be 128 B");
+
+struct alignas(16) RasterPart {  // first 80 B of Rec
+    int32_t A[3];
+    int32_t B[3];
+    int64_t C[3];
+    uint16_t i0, i1, j0, j1;
+    int32_t face;
+    float fx0, fy0, z0, za, zb;
+};
+static_assert(sizeof(RasterPart) == 80, "RasterPart must be 80 B");
+
+__host__ __device__ inline int64_t rec_index(int F, int f, int s)
+{
+    return s == 0 ? (int64_t)f : (int64_t)F + (int64_t)kExtraPerFace * f + (s - 1);
+}
+
+__device__ inline void set_empty(Rec *r, int face)
+{
+    r->i0 = 1; r->i1 = 0; r->j0 = 1; r->j1 = 0;
+    r->face = face;
+}
+
+// R1..R4 for one (sub-)triangle: writes *r, returns true if non-empty.
+__device__ inline bool make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, Rec *r)
+{
+    const float hw = 0.5f * (float)W, hh = 0.5f * (float)H;
+    int32_t X[3], Y[3];
+    float zw[3], iwv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float iw = 1.0f / v[k][3];
+        float xn = v[k][0] * iw, yn = v[k][1] * iw, zn = v[k][2] * iw;
+        float xw = (xn + 1.0f) * hw, yw = (yn + 1.0f) * hh;
+        zw[k] = zn * 0.5f + 0.5f;
+        X[k] = (int32_t)__builtin_rintf(xw * 256.0f);
+        Y[k] = (int32_t)__builtin_rintf(yw * 256.0f);
+        iwv[k] = iw;
+    }
+    int64_t A[3], B[3], C[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int a = (k + 1) % 3, b = (k + 2) % 3;
+        A[k] = (int64_t)Y[a] - Y[b];
+        B[k] = (int64_t)X[b] - X[a];
+        C[k] = -(A[k] * X[a] + B[k] * Y[a]);
+    }
+    const int64_t D = A[0] * X[0] + B[0] * Y[0] + C[0];
+    if (D == 0) { set_empty(r, face); return false; }
+    if (D < 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { A[k] = -A[k]; B[k] = -B[k]; C[k] = -C[k]; }
+    }
+    int32_t xmin = min(X[0], min(X[1], X[2])), xmax = max(X[0], max(X[1], X[2]));
+    int32_t ymin = min(Y[0], min(Y[1], Y[2])), ymax = max(Y[0], max(Y[1], Y[2]));
+    int64_t i0 = ((int64_t)xmin - 128 + 255) >> 8, i1 = ((int64_t)xmax - 128) >> 8;  // arithmetic shift = floor
+    int64_t j0 = ((int64_t)ymin - 128 + 255) >> 8, j1 = ((int64_t)ymax - 128) >> 8;
+    i0 = i0 < 0 ? 0 : i0;
+    j0 = j0 < 0 ? 0 : j0;
+    i1 = i1 > W - 1 ? W - 1 : i1;
+    j1 = j1 > H - 1 ? H - 1 : j1;
+    if (i0 > i1 || j0 > j1) { set_empty(r, face); return false; }
+    const float fx0 = (float)X[0] * 0.00390625f, fy0 = (float)Y[0] * 0.00390625f;
+    const float dx1 = (float)X[1] * 0.00390625f - fx0, dy1 = (float)Y[1] * 0.00390625f - fy0;
+    const float dx2 = (float)X[2] * 0.00390625f - fx0, dy2 = (float)Y[2] * 0.00390625f - fy0;
+    const float dz1 = zw[1] - zw[0], dz2 = zw[2] - zw[0];
+    const float det = (float)D * (1.0f / 65536.0f);
+    Rec out;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { out.A[k] = (int32_t)A[k]; out.B[k] = (int32_t)B[k]; out.C[k] = C[k]; }
+    out.i0 = (uint16_t)i0; out.i1 = (uint16_t)i1; out.j0 = (uint16_t)j0; out.j1 = (uint16_t)j1;
+    out.face = face;
+    out.fx0 = fx0; out.fy0 = fy0; out.z0 = zw[0];
+    out.za = (dz1 * dy2 - dz2 * dy1) / det;
+    out.zb = (dx1 * dz2 - dx2 * dz1) / det;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        out.iw[k] = iwv[k];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) out.basis[k * 3 + i] = basis[k][i];
+    }
+    *r = out;
+    return true;
+}
+
+// R3: exact edge values at pixel centre (i,j)
+template <typename R>
+__device__ __forceinline__ void edge_values(const R &r, int i, int j, int64_t E[3])
+{
+    const int64_t px = (int64_t)i * 256 + 128, py = (int64_t)j * 256 + 128;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E[k] = (int64_t)r.A[k] * px + (int64_t)r.B[k] * py + r.C[k];
+}
+
+// R3 top-left rule
+template <typename R>
+__device__ __forceinline__ bool inside(const R &r, const int64_t E[3])
+{
+    bool in = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool owned = r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0);
+        in = in && (E[k] > 0 || (E[k] == 0 && owned));
+    }
+    return in;
+}
+
+// R4: 24-bit depth of the sample, false if outside [0,1] or not nearer than the cleared depth
+template <typename R>
+__device__ __forceinline__ bool sample_depth(const R &r, int i, int j, uint32_t &d)
+{
+    const float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
+    const float zw = (r.za * (fx - r.fx0) + r.zb * (fy - r.fy0)) + r.z0;
+    if (!(zw >= 0.0f && zw <= 1.0f)) return false;
+    const uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
+    if (q >= kDepthMax) return false;
+    d = q;
+    return true;
+}
+
+// R6: perspective-correct parent barycentrics from edge values (or sums of two edge values)
+__device__ __forceinline__ bool parent_lambda(const Rec &r, const int64_t E[3], float lam[3])
+{
+    const float a0 = (float)E[0] * r.iw[0], a1 = (float)E[1] * r.iw[1], a2 = (float)E[2] * r.iw[2];
+    const float s = (a0 + a1) + a2;
+    if (s == 0.0f) return false;
+    const float m0 = a0 / s, m1 = a1 / s, m2 = a2 / s;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
+    return true;
+}
+
+}  // namespace dirt

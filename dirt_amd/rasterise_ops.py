@@ -1,0 +1,194 @@
+"""PyTorch mirror of the reference's op surface, dirt/rasterise_ops.py.
+
+Same function names, argument order, defaults and shape inference as the reference
+(dirt/rasterise_ops.py:10-203); TensorFlow graph ops become eager PyTorch-ROCm calls into
+libdirt_mi355x.so, and the op gets the gradient the reference never registered:
+`rasterise` / `rasterise_batch` are differentiable w.r.t. background, vertices and vertex_colors.
+
+Differences from the reference, all deliberate:
+  * `camera_pos` is optional (default None): the fork made it a mandatory positional argument of
+    `rasterise` (rasterise_ops.py:10) but forgot it in `rasterise_batch` (:84-88), so every
+    upstream-style caller raised; here both call forms work.
+  * channels may be 1..8 (the reference CHECK-aborts unless 1 or 3, csrc/hwc.h:27), so the 7-channel
+    deferred G-buffer (BASELINE config 4) is one call instead of three.
+  * errors are exceptions, never process aborts (csrc/rasterise_egl.cpp:85-503 LOG(FATAL)).
+There is no CPU path: the op requires a HIP device and raises if the native library is missing.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+__all__ = [
+    "rasterise", "rasterise_batch", "rasterise_grad",
+    "oceanic_no_cloud", "oceanic_simple_proxy", "oceanic_still_cloud", "oceanic_opt_flow", "hill",
+]
+
+
+def _device_of(*xs):
+    for x in xs:
+        if isinstance(x, torch.Tensor) and x.device.type == "cuda":
+            return x.device
+    if not torch.cuda.is_available():
+        raise RuntimeError("dirt_amd.rasterise requires a ROCm/HIP GPU: there is no CPU implementation")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _as_tensor(x, dtype, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype)
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
+
+
+class _RasteriseFunction(torch.autograd.Function):
+    """Rasterise op (csrc/rasterise_egl.cpp:33-53) with its registered gradient."""
+
+    @staticmethod
+    def forward(ctx, background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
+                bin_capacity):
+        B, V, F = vertices.shape[0], vertices.shape[1], faces.shape[1]
+        H, W, C = height, width, channels
+        dev = vertices.device
+        lib = _lib.load()
+        saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, bin_capacity)
+        pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+        gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+        saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
+        scratch = torch.empty((max(scratch_bytes, 1),), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            cam = camera_pos.data_ptr() if camera_pos is not None else None
+            _lib.check(lib.dirt_rasterise_fwd(
+                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
+                B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
+                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, stream))
+        ctx.save_for_backward(vertices, vertex_colors, faces, pixels, gbuffer, saved)
+        ctx.dims = (B, H, W, C, V, F)
+        ctx.shader_id = shader_id
+        ctx.mark_non_differentiable(gbuffer)
+        return pixels, gbuffer
+
+    @staticmethod
+    def backward(ctx, grad_pixels, _grad_gbuffer):
+        if ctx.shader_id != _lib.SHADER_GOURAUD:
+            raise RuntimeError("only the Gouraud fragment program has a gradient (the reference registers none)")
+        vertices, vertex_colors, faces, pixels, gbuffer, saved = ctx.saved_tensors
+        B, H, W, C, V, F = ctx.dims
+        dev = vertices.device
+        grad_pixels = grad_pixels.to(dtype=torch.float32).contiguous()
+        grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
+        grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
+        grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(lib.dirt_rasterise_bwd(
+                vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), pixels.data_ptr(),
+                grad_pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(),
+                B, H, W, C, V, F, grad_vertices.data_ptr(), grad_colors.data_ptr(), grad_background.data_ptr(),
+                stream))
+        return grad_background, grad_vertices, grad_colors, None, None, None, None, None, None, None
+
+
+def _check_shapes(background, vertices, vertex_colors, faces, H, W, C):
+    # messages follow csrc/rasterise_egl.cpp:310-336
+    if background.dim() != 4 or tuple(background.shape[1:]) != (H, W, C):
+        raise ValueError("Rasterise expects background_tensor to be 4D, and bgcolor.shape == [None, height, width, channels]")
+    if vertices.dim() != 3 or vertices.shape[2] != 4:
+        raise ValueError("Rasterise expects vertices to be 3D, and vertices.shape[2] == 4")
+    if vertex_colors.dim() != 3 or vertex_colors.shape[1] != vertices.shape[1] or vertex_colors.shape[2] != C:
+        raise ValueError("Rasterise expects vertex_colors to be 3D, and vertex_colors.shape == [None, vertices.shape[1], channels]")
+    if faces.dim() != 3 or faces.shape[2] != 3:
+        raise ValueError("Rasterise expects faces to be 3D, and faces.shape[2] == 3")
+    B = vertices.shape[0]
+    if background.shape[0] != B or vertex_colors.shape[0] != B or faces.shape[0] != B:
+        raise ValueError("Rasterise expects all arguments to have same leading (batch) dimension")
+    if not (C >= 1 and C <= _lib.MAX_CHANNELS):
+        raise ValueError("Rasterise expects 1 <= channels <= %d" % _lib.MAX_CHANNELS)
+
+
+def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
+                       bin_capacity=0, return_gbuffer=False):
+    dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
+    background = _as_tensor(background, torch.float32, dev).contiguous()
+    vertices = _as_tensor(vertices, torch.float32, dev).contiguous()
+    vertex_colors = _as_tensor(vertex_colors, torch.float32, dev).contiguous()
+    faces = _as_tensor(faces, torch.int32, dev).contiguous()
+    if camera_pos is not None:
+        camera_pos = _as_tensor(camera_pos, torch.float32, dev).contiguous().reshape(-1)
+        if camera_pos.numel() < 8:
+            raise ValueError("camera_pos must hold at least 8 floats (csrc/rasterise_egl.cpp:323)")
+    _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
+    pixels, gbuffer = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos,
+                                               int(height), int(width), int(channels), shader_id, int(bin_capacity))
+    return (pixels, gbuffer) if return_gbuffer else pixels
+
+
+def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None, channels=None,
+              name=None):
+    """Rasterises the given `vertices` and `faces` over `background` (reference dirt/rasterise_ops.py:10-54).
+
+    Args:
+        background: float32 [height, width, channels] image to render over (top row first)
+        vertices: float32 [vertex count, 4] OpenGL clip-space positions
+        vertex_colors: float32 [vertex count, channels]; interpolated perspective-correctly (Gouraud)
+        faces: int32 [face count, 3] indices into `vertices`
+        camera_pos: optional float32 [>=8]; only read by procedural fragment programs
+        height, width, channels: may be None, then inferred from `background`'s shape
+        name: ignored (TensorFlow name scope in the reference)
+
+    Returns:
+        float32 [height, width, channels] pixels, differentiable w.r.t. background, vertices, vertex_colors.
+    """
+    del name
+    bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
+    if height is None:
+        height = int(bshape[0])
+    if width is None:
+        width = int(bshape[1])
+    if channels is None:
+        channels = int(bshape[2])
+    dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
+    background = _as_tensor(background, torch.float32, dev)
+    vertices = _as_tensor(vertices, torch.float32, dev)
+    vertex_colors = _as_tensor(vertex_colors, torch.float32, dev)
+    faces = _as_tensor(faces, torch.int32, dev)
+    return _rasterise_batched(background[None], vertices[None], vertex_colors[None], faces[None], camera_pos,
+                              height, width, channels, _lib.SHADER_GOURAUD)[0]
+
+
+def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
+                    channels=None, name=None):
+    """Rasterises a batch of meshes with equal vertex and face counts (reference dirt/rasterise_ops.py:57-88).
+
+    Conceptually `torch.stack([rasterise(bg_i, v_i, c_i, f_i) for ...])`; every argument carries a leading
+    batch dimension and faces index the vertices of their own frame.
+    """
+    del name
+    bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
+    if height is None:
+        height = int(bshape[1])
+    if width is None:
+        width = int(bshape[2])
+    if channels is None:
+        channels = int(bshape[3])
+    return _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels,
+                              _lib.SHADER_GOURAUD)
+
+
+def _procedural(opname):
+    def op(background, vertices, vertex_colors, faces, camera_pos, height=None, width=None, channels=None,
+           name=None):
+        raise NotImplementedError(
+            "%s: procedural fragment program not implemented yet on MI355X (SURVEY 8f-4)" % opname)
+    op.__name__ = opname
+    op.__doc__ = "Reference dirt/rasterise_ops.py procedural op `%s` (SURVEY 8f-4)." % opname
+    return op
+
+
+rasterise_grad = _procedural("rasterise_grad")
+oceanic_no_cloud = _procedural("oceanic_no_cloud")
+oceanic_simple_proxy = _procedural("oceanic_simple_proxy")
+oceanic_still_cloud = _procedural("oceanic_still_cloud")
+oceanic_opt_flow = _procedural("oceanic_opt_flow")
+hill = _procedural("hill")

@@ -1,0 +1,66 @@
+"""Preallocated, graph-capturable rasterise forward/backward for fixed shapes.
+
+`rasterise` / `rasterise_batch` allocate their outputs and workspace per call and go through autograd;
+that is the drop-in surface.  A serving or training loop that renders the same shapes every step can
+instead hold a `RasteriseSession`: buffers are allocated once and each call is a single ctypes call into
+the C ABI, so a whole forward+backward step can be captured into a HIP graph (torch.cuda.CUDAGraph) and
+replayed without host launch overhead.  Results are identical to the autograd path (same kernels).
+"""
+import torch
+
+from . import _lib
+
+
+class RasteriseSession:
+    def __init__(self, B, H, W, C, V, F, device=None, bin_capacity=0, shader_id=_lib.SHADER_GOURAUD):
+        self.dims = (B, H, W, C, V, F)
+        self.shader_id = shader_id
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.bin_capacity = int(bin_capacity)
+        saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, self.bin_capacity)
+        self.saved_bytes, self.scratch_bytes = saved_bytes, scratch_bytes
+        dev = self.device
+        self.pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+        self.gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+        self.saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
+        self.scratch = torch.empty((max(scratch_bytes, 1),), dtype=torch.uint8, device=dev)
+        self.grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
+        self.grad_vertex_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
+        self.grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+        self._lib = _lib.load()
+        self._inputs = None
+
+    def _check(self, t, shape, dtype):
+        if t.device != self.device or t.dtype != dtype or tuple(t.shape) != shape or not t.is_contiguous():
+            raise ValueError("RasteriseSession expects a contiguous %s %s tensor on %s, got %s %s on %s"
+                             % (dtype, shape, self.device, t.dtype, tuple(t.shape), t.device))
+
+    def forward(self, background, vertices, vertex_colors, faces, camera_pos=None):
+        B, H, W, C, V, F = self.dims
+        self._check(background, (B, H, W, C), torch.float32)
+        self._check(vertices, (B, V, 4), torch.float32)
+        self._check(vertex_colors, (B, V, C), torch.float32)
+        self._check(faces, (B, F, 3), torch.int32)
+        self._inputs = (background, vertices, vertex_colors, faces)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        cam = camera_pos.data_ptr() if camera_pos is not None else None
+        _lib.check(self._lib.dirt_rasterise_fwd(
+            background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
+            B, H, W, C, V, F, self.shader_id, self.pixels.data_ptr(), self.gbuffer.data_ptr(),
+            self.saved.data_ptr(), self.saved_bytes, self.scratch.data_ptr(), self.scratch_bytes,
+            self.bin_capacity, stream))
+        return self.pixels
+
+    def backward(self, grad_pixels):
+        if self._inputs is None:
+            raise RuntimeError("RasteriseSession.backward called before forward")
+        B, H, W, C, V, F = self.dims
+        self._check(grad_pixels, (B, H, W, C), torch.float32)
+        _, vertices, vertex_colors, faces = self._inputs
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self._lib.dirt_rasterise_bwd(
+            vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), self.pixels.data_ptr(),
+            grad_pixels.data_ptr(), self.gbuffer.data_ptr(), self.saved.data_ptr(), B, H, W, C, V, F,
+            self.grad_vertices.data_ptr(), self.grad_vertex_colors.data_ptr(), self.grad_background.data_ptr(),
+            stream))
+        return self.grad_background, self.grad_vertices, self.grad_vertex_colors

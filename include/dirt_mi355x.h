@@ -1,0 +1,104 @@
+/*
+ * dirt_mi355x.h -- C ABI of the MI355X-native dirt rasteriser (libdirt_mi355x.so).
+ *
+ * Drop-in boundary for the reference's TensorFlow custom ops in librasterise.so
+ * (loaded by tf.load_op_library at dirt/rasterise_ops.py:7):
+ *
+ *   dirt_rasterise_fwd  replaces  REGISTER_OP("Rasterise")           csrc/rasterise_egl.cpp:33-53
+ *                                 RasteriseOpGpu::Compute            csrc/rasterise_egl.cpp:284-514
+ *                                 upload_background/download_pixels  csrc/rasterise_egl.cu:16-129
+ *   dirt_rasterise_bwd  replaces  launch_grad_assembly (declared,    csrc/rasterise_grad_common.h:19-24
+ *                                 never defined in the fork) -- the gradient DIRT registers upstream
+ *                                 for "Rasterise"; the fork's REGISTER_OP("RasteriseGrad")
+ *                                 (csrc/rasterise_grad_egl.cpp:33-53) is a forward render
+ *   dirt_last_error     replaces  OP_REQUIRES(..., errors::InvalidArgument(...)) messages,
+ *                                 csrc/rasterise_egl.cpp:310-336 (the reference aborts on everything
+ *                                 else via LOG(FATAL)/CHECK; this ABI never aborts)
+ *
+ * Conventions
+ *   - every tensor pointer is a DEVICE pointer to a dense row-major array (HBM of the current HIP device);
+ *   - float32 data, int32 faces; shapes use the reference's batch-leading layout
+ *       background    [B,H,W,C]   top row first (rasterise_egl.cu:29)
+ *       vertices      [B,V,4]     OpenGL clip space x,y,z,w (README.md:131)
+ *       vertex_colors [B,V,C]
+ *       faces         [B,F,3]     indices into the same frame's vertices (base vertex b*V, rasterise_egl.cpp:457)
+ *       pixels        [B,H,W,C]   output
+ *   - outputs are caller-owned; work is enqueued asynchronously on `stream` (a hipStream_t, 0 = null stream);
+ *   - `saved` is the state the backward needs (per-face setup records); `scratch` is forward-only
+ *     (tile bins).  Query their sizes with dirt_workspace_sizes; the caller owns both.
+ *   - channels C may be 1..DIRT_MAX_CHANNELS (the reference accepts 1 or 3, csrc/hwc.h:27).
+ *
+ * Return codes: DIRT_OK, DIRT_EINVAL (bad shape/argument; message in dirt_last_error()),
+ * DIRT_EHIP (a HIP runtime error).  Out-of-range face indices cull the face (the reference reads
+ * out of bounds); dirt_check_faces() reports them on request.
+ */
+#ifndef DIRT_MI355X_H
+#define DIRT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DIRT_OK 0
+#define DIRT_EINVAL 1
+#define DIRT_EFACE 2
+#define DIRT_EHIP 3
+
+#define DIRT_MAX_CHANNELS 8
+#define DIRT_MAX_DIM 8192
+
+/* fragment programs (shader_id); 0 = Gouraud (README.md:134-137) */
+#define DIRT_SHADER_GOURAUD 0
+#define DIRT_SHADER_OCEANIC_HORIZON 1 /* csrc/shaders.cpp:1668-1919 (the fork's bound program) */
+
+/* ABI version, bumped on any signature change */
+int dirt_abi_version(void);
+
+/* Byte sizes of the caller-provided buffers for one call.
+ * bin_capacity = number of (tile, triangle) bin entries the scratch can hold (<=0: default policy). */
+int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_capacity,
+                         size_t *saved_bytes, size_t *scratch_bytes);
+
+/* Forward: pixels = Rasterise(background, vertices, vertex_colors, faces).
+ * gbuffer [B,H,W] int32 receives the per-pixel visible setup-record index (-1 = background),
+ * which together with `saved` is what dirt_rasterise_bwd consumes.
+ * camera_pos: device pointer to >= 8 floats, used only by shader_id != 0 (may be NULL for Gouraud). */
+int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
+                       const int32_t *faces, const float *camera_pos,
+                       int B, int H, int W, int C, int V, int F, int shader_id,
+                       float *pixels, int32_t *gbuffer,
+                       void *saved, size_t saved_bytes, void *scratch, size_t scratch_bytes,
+                       int64_t bin_capacity, void *stream);
+
+/* Backward: given grad_pixels = dL/dpixels, writes dL/dvertices [B,V,4] (z component is 0),
+ * dL/dvertex_colors [B,V,C] and dL/dbackground [B,H,W,C].  All three outputs are fully
+ * overwritten.  Filter-based (DIRT/OpenDR) derivative, DESIGN.md section 4. */
+int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces,
+                       const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
+                       const void *saved,
+                       int B, int H, int W, int C, int V, int F,
+                       float *grad_vertices, float *grad_vertex_colors, float *grad_background,
+                       void *stream);
+
+/* Debug check (synchronises `stream`): returns DIRT_EFACE if any face index is outside [0,V). */
+int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, size_t scratch_bytes, void *stream);
+
+/* Optional per-kernel timing with HIP events around every launch (used by bench.py for the roofline).
+ * dirt_profile_enable(1) clears and starts recording, (0) clears and stops.  dirt_profile_read
+ * synchronises the recorded events of kernel `kernel_id` (0..DIRT_NUM_KERNELS-1) and returns its name,
+ * launch count and summed duration.  Not thread-safe; do not enable during hipGraph capture. */
+#define DIRT_NUM_KERNELS 5
+int dirt_profile_enable(int enable);
+int dirt_profile_read(int kernel_id, const char **name, int *launches, double *total_ms);
+
+/* Thread-local message for the last non-OK return on this thread. */
+const char *dirt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DIRT_MI355X_H */

@@ -1,0 +1,491 @@
+/*
+ * dirt_oracle.c -- CPU ORACLE for the dirt rasterise hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the checker, never the product: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product path (dirt_amd/) never links it.
+ *
+ * It restates, as plain single-pass C loops, what the reference's `Rasterise` op computes
+ * through the OpenGL fixed-function pipeline:
+ *   - op signature / shapes / batching     : csrc/rasterise_egl.cpp:33-53, 309-339
+ *   - per-frame draw in face index order   : csrc/rasterise_egl.cpp:440-458 (glDrawElementsBaseVertex,
+ *                                             base vertex b*V -> faces index the frame's own vertices)
+ *   - depth test LESS on a DEPTH24 buffer   : csrc/rasterise_egl.cpp:194 (GL_DEPTH_TEST), :248 (DEPTH24_STENCIL8),
+ *     cleared to 1.0 per frame               : csrc/rasterise_egl.cpp:449
+ *   - vertex stage = clip-space passthrough : csrc/shaders.cpp:16-34
+ *   - Gouraud colour (perspective-correct)  : README.md:134-137, dirt/rasterise_ops.py:25-26
+ *   - background where uncovered, rows flipped to top-row-first:
+ *                                             csrc/rasterise_egl.cu:16-51 (upload), :78-104 (download)
+ *   - no face culling, no blending          : (no glEnable(GL_CULL_FACE)/GL_BLEND anywhere in csrc/)
+ * and the gradient contract of csrc/rasterise_grad_common.h:19-24 (grad_vertices, grad_vertex_colors,
+ * grad_background from pixels + grad_pixels), whose algorithm the fork lost; the
+ * backward rule is DIRT's filter-based derivative (README.md:146-147) as specified in DESIGN.md §4.
+ *
+ * PARITY STATUS: the GL driver's exact rasterisation arithmetic is closed source and the reference
+ * ships no golden vectors, so the driver-level rules below are *chosen*  and
+ * pinned by analytic known-answer tests derived from the reference (README.md:27-70 square, the
+ * rasterise_tests.py cylinder invariants) -- "parity pinned by KATs; driver arithmetic unpinned".
+ *
+ * Raster rules (identical in the HIP path):
+ *   R1 vertex: iw=1/w; window xw=(x*iw+1)*(W/2), yw=(y*iw+1)*(H/2) (GL y up), zw=(z*iw)*0.5+0.5
+ *   R2 snap:   X=rint(xw*256), Y=rint(yw*256)   (8 sub-pixel bits)
+ *   R3 edges:  E_k(P) = A_k*Px + B_k*Py + C_k, exact int64, sample at pixel centre (256i+128, 256j+128);
+ *              orientation normalised so the interior is positive; top-left rule: an E_k==0 sample is
+ *              inside iff edge k is "left" (A_k>0) or "top" (A_k==0 && B_k<0).
+ *   R4 depth:  plane through the snapped vertices, float32, zw in [0,1]; d=(uint)(zw*(2^24-1)+0.5),
+ *              passes iff d < 2^24-1 and ((d<<32)|face) is the minimum so far (LESS, first face wins ties)
+ *   R5 clip:   faces with every vertex strictly inside the guard band (w>0, |x|<=gx*w, |y|<=gy*w,
+ *              gx=32768/W, gy=32768/H) are rasterised directly (near/far by the per-sample zw test);
+ *              others are clipped (Sutherland-Hodgman, float32) against z>=-w and the guard planes and
+ *              fan-triangulated; sub-triangle s>0 of face f lives at record index F+5f+(s-1).
+ *   R6 colour: lambda_k = a_k/((a_0+a_1)+a_2), a_k=float(E_k)*iw_k, mapped through the clip basis;
+ *              colour = (l0*c0 + l1*c1) + l2*c2.
+ *
+ * Compile with -ffp-contract=off (Makefile): every float operation above is one IEEE op, so the HIP
+ * kernels (also built with -ffp-contract=off) reproduce coverage, depth and face ids bit-exactly.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define SUBPIX 256
+#define MAX_SUB 6 /* a triangle clipped by 5 planes has <= 8 vertices -> <= 6 fan triangles */
+#define MAX_POLY 9
+#define DEPTH_MAX 16777215u
+
+typedef struct {
+    int32_t A[3], B[3];
+    int64_t C[3];
+    int32_t i0, j0, i1, j1; /* inclusive pixel bbox; empty if i0>i1 */
+    int32_t face;
+    float fx0, fy0, z0, za, zb;
+    float iw[3];
+    float basis[9]; /* row k = parent barycentric of sub-vertex k */
+} orc_rec;
+
+static int64_t floor_div256(int64_t v) { return v >= 0 ? v / 256 : -((-v + 255) / 256); }
+
+/* R1-R4 for one (sub-)triangle given clip coords (x,y,z,w) of three vertices and their parent basis.
+ * Returns 1 if the triangle produces a non-empty record. */
+static int make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, orc_rec *r)
+{
+    const float hw = 0.5f * (float)W, hh = 0.5f * (float)H;
+    int32_t X[3], Y[3];
+    float zw[3];
+    for (int k = 0; k < 3; ++k) {
+        float iw = 1.0f / v[k][3];
+        float xn = v[k][0] * iw, yn = v[k][1] * iw, zn = v[k][2] * iw;
+        float xw = (xn + 1.0f) * hw, yw = (yn + 1.0f) * hh;
+        zw[k] = zn * 0.5f + 0.5f;
+        X[k] = (int32_t)rintf(xw * 256.0f);
+        Y[k] = (int32_t)rintf(yw * 256.0f);
+        r->iw[k] = iw;
+        for (int i = 0; i < 3; ++i) r->basis[k * 3 + i] = basis[k][i];
+    }
+    int64_t A[3], B[3], C[3];
+    for (int k = 0; k < 3; ++k) {
+        int a = (k + 1) % 3, b = (k + 2) % 3;
+        A[k] = (int64_t)Y[a] - Y[b];
+        B[k] = (int64_t)X[b] - X[a];
+        C[k] = -(A[k] * X[a] + B[k] * Y[a]);
+    }
+    int64_t D = A[0] * X[0] + B[0] * Y[0] + C[0];
+    if (D == 0) return 0;
+    int64_t Dsigned = D;
+    if (D < 0) {
+        for (int k = 0; k < 3; ++k) { A[k] = -A[k]; B[k] = -B[k]; C[k] = -C[k]; }
+    }
+    for (int k = 0; k < 3; ++k) { r->A[k] = (int32_t)A[k]; r->B[k] = (int32_t)B[k]; r->C[k] = C[k]; }
+    int32_t xmin = X[0], xmax = X[0], ymin = Y[0], ymax = Y[0];
+    for (int k = 1; k < 3; ++k) {
+        if (X[k] < xmin) xmin = X[k];
+        if (X[k] > xmax) xmax = X[k];
+        if (Y[k] < ymin) ymin = Y[k];
+        if (Y[k] > ymax) ymax = Y[k];
+    }
+    int64_t i0 = floor_div256((int64_t)xmin - 128 + 255), i1 = floor_div256((int64_t)xmax - 128);
+    int64_t j0 = floor_div256((int64_t)ymin - 128 + 255), j1 = floor_div256((int64_t)ymax - 128);
+    if (i0 < 0) i0 = 0;
+    if (j0 < 0) j0 = 0;
+    if (i1 > W - 1) i1 = W - 1;
+    if (j1 > H - 1) j1 = H - 1;
+    if (i0 > i1 || j0 > j1) return 0;
+    r->i0 = (int32_t)i0; r->i1 = (int32_t)i1; r->j0 = (int32_t)j0; r->j1 = (int32_t)j1;
+    r->face = face;
+    /* depth plane through the snapped vertices (R4) */
+    float fx0 = (float)X[0] * 0.00390625f, fy0 = (float)Y[0] * 0.00390625f;
+    float dx1 = (float)X[1] * 0.00390625f - fx0, dy1 = (float)Y[1] * 0.00390625f - fy0;
+    float dx2 = (float)X[2] * 0.00390625f - fx0, dy2 = (float)Y[2] * 0.00390625f - fy0;
+    float dz1 = zw[1] - zw[0], dz2 = zw[2] - zw[0];
+    float det = (float)Dsigned * (1.0f / 65536.0f);
+    r->za = (dz1 * dy2 - dz2 * dy1) / det;
+    r->zb = (dx1 * dz2 - dx2 * dz1) / det;
+    r->fx0 = fx0; r->fy0 = fy0; r->z0 = zw[0];
+    return 1;
+}
+
+static int finite4(const float *v) { return isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]); }
+
+/* plane distances for R5 clipping, in fixed order */
+static float plane_dist(int p, const float *v, float gx, float gy)
+{
+    switch (p) {
+    case 0: return v[2] + v[3];
+    case 1: return gx * v[3] + v[0];
+    case 2: return gx * v[3] - v[0];
+    case 3: return gy * v[3] + v[1];
+    default: return gy * v[3] - v[1];
+    }
+}
+
+/* Set up face f of one frame: fills recs[0..nsub-1] (empty ones have i0>i1). Returns nsub (0 = culled). */
+static int setup_face(const float *verts, const int32_t *face3, int V, int W, int H, int f, orc_rec recs[MAX_SUB])
+{
+    for (int s = 0; s < MAX_SUB; ++s) { recs[s].i0 = 1; recs[s].i1 = 0; recs[s].face = f; }
+    float v[3][4];
+    for (int k = 0; k < 3; ++k) {
+        int32_t vi = face3[k];
+        if (vi < 0 || vi >= V) return 0;
+        for (int c = 0; c < 4; ++c) v[k][c] = verts[(int64_t)vi * 4 + c];
+        if (!finite4(v[k])) return 0;
+    }
+    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+    int fast = 1;
+    for (int k = 0; k < 3; ++k) {
+        float w = v[k][3];
+        if (!(w > 0.0f && fabsf(v[k][0]) <= gx * w && fabsf(v[k][1]) <= gy * w)) fast = 0;
+    }
+    if (fast) {
+        const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
+        make_record((const float(*)[4])v, id, W, H, f, &recs[0]);
+        return 1;
+    }
+    /* R5: Sutherland-Hodgman against near + 4 guard planes, carrying the parent basis */
+    float poly[MAX_POLY][7], tmp[MAX_POLY][7];
+    int n = 3;
+    for (int k = 0; k < 3; ++k) {
+        for (int c = 0; c < 4; ++c) poly[k][c] = v[k][c];
+        for (int i = 0; i < 3; ++i) poly[k][4 + i] = (i == k) ? 1.0f : 0.0f;
+    }
+    for (int p = 0; p < 5; ++p) {
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const float *a = poly[i], *c = poly[(i + 1) % n];
+            float da = plane_dist(p, a, gx, gy), dc = plane_dist(p, c, gx, gy);
+            int ina = da >= 0.0f, inc = dc >= 0.0f;
+            if (ina) { memcpy(tmp[m], a, sizeof(tmp[m])); ++m; }
+            if (ina != inc) {
+                float t = da / (da - dc);
+                for (int q = 0; q < 7; ++q) tmp[m][q] = a[q] + t * (c[q] - a[q]);
+                ++m;
+            }
+        }
+        n = m;
+        if (n < 3) return 0;
+        memcpy(poly, tmp, sizeof(float) * 7 * (size_t)n);
+    }
+    for (int i = 0; i < n; ++i)
+        if (!(poly[i][3] > 0.0f)) return 0;
+    int nsub = n - 2;
+    for (int s = 0; s < nsub; ++s) {
+        float sv[3][4], sb[3][3];
+        const int idx[3] = {0, s + 1, s + 2};
+        for (int k = 0; k < 3; ++k) {
+            for (int c = 0; c < 4; ++c) sv[k][c] = poly[idx[k]][c];
+            for (int i = 0; i < 3; ++i) sb[k][i] = poly[idx[k]][4 + i];
+        }
+        make_record((const float(*)[4])sv, (const float(*)[3])sb, W, H, f, &recs[s]);
+    }
+    return nsub;
+}
+
+static inline int rec_nonempty(const orc_rec *r) { return r->i0 <= r->i1; }
+
+static inline void edge_values(const orc_rec *r, int i, int j, int64_t E[3])
+{
+    int64_t px = (int64_t)i * 256 + 128, py = (int64_t)j * 256 + 128;
+    for (int k = 0; k < 3; ++k) E[k] = (int64_t)r->A[k] * px + (int64_t)r->B[k] * py + r->C[k];
+}
+
+static inline int inside(const orc_rec *r, const int64_t E[3])
+{
+    for (int k = 0; k < 3; ++k) {
+        if (E[k] > 0) continue;
+        if (E[k] == 0 && (r->A[k] > 0 || (r->A[k] == 0 && r->B[k] < 0))) continue;
+        return 0;
+    }
+    return 1;
+}
+
+/* R4: returns 1 and the 24-bit depth if the sample passes the depth-range test */
+static inline int sample_depth(const orc_rec *r, int i, int j, uint32_t *d)
+{
+    float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
+    float zw = (r->za * (fx - r->fx0) + r->zb * (fy - r->fy0)) + r->z0;
+    if (!(zw >= 0.0f && zw <= 1.0f)) return 0;
+    uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
+    if (q >= DEPTH_MAX) return 0;
+    *d = q;
+    return 1;
+}
+
+/* R6: perspective-correct parent barycentrics from (possibly doubled) edge values */
+static inline int parent_lambda(const orc_rec *r, const int64_t E[3], float lam[3])
+{
+    float a0 = (float)E[0] * r->iw[0], a1 = (float)E[1] * r->iw[1], a2 = (float)E[2] * r->iw[2];
+    float s = (a0 + a1) + a2;
+    if (s == 0.0f) return 0;
+    float m0 = a0 / s, m1 = a1 / s, m2 = a2 / s;
+    for (int i = 0; i < 3; ++i) lam[i] = (m0 * r->basis[0 * 3 + i] + m1 * r->basis[1 * 3 + i]) + m2 * r->basis[2 * 3 + i];
+    return 1;
+}
+
+static inline int64_t rec_index(int F, int f, int s) { return s == 0 ? f : (int64_t)F + 5 * (int64_t)f + (s - 1); }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Setup for a whole frame: recs has 6F slots, nsub F entries */
+static int setup_frame(const float *verts, const int32_t *faces, int V, int F, int W, int H, orc_rec *recs, int32_t *nsub)
+{
+    int bad = 0;
+    for (int64_t i = 0; i < 6 * (int64_t)F; ++i) { recs[i].i0 = 1; recs[i].i1 = 0; recs[i].face = -1; }
+    for (int f = 0; f < F; ++f) {
+        orc_rec tmp[MAX_SUB];
+        const int32_t *f3 = faces + 3 * (int64_t)f;
+        for (int k = 0; k < 3; ++k)
+            if (f3[k] < 0 || f3[k] >= V) bad = 1;
+        int n = setup_face(verts, f3, V, W, H, f, tmp);
+        nsub[f] = n;
+        for (int s = 0; s < n; ++s) recs[rec_index(F, f, s)] = tmp[s];
+    }
+    return bad;
+}
+
+/* Forward: pixels [B,H,W,C] (rows top-first), gbuffer [B,H,W] record index or -1.
+ * Returns 0, or 2 if a face index was out of range (such faces are culled). */
+int oracle_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
+                         const int32_t *faces, int B, int H, int W, int C, int V, int F,
+                         float *pixels, int32_t *gbuffer, int nthreads)
+{
+    int status = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    orc_rec *recs = (orc_rec *)malloc(sizeof(orc_rec) * 6 * (size_t)(F > 0 ? F : 1));
+    int32_t *nsub = (int32_t *)malloc(sizeof(int32_t) * (size_t)(F > 0 ? F : 1));
+    uint64_t *keys = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)H * W);
+    int32_t *rbuf = (int32_t *)malloc(sizeof(int32_t) * (size_t)H * W);
+    for (int b = 0; b < B; ++b) {
+        const float *vb = vertices + (int64_t)b * V * 4;
+        const float *cb = vertex_colors + (int64_t)b * V * C;
+        const int32_t *fb = faces + (int64_t)b * F * 3;
+        if (setup_frame(vb, fb, V, F, W, H, recs, nsub)) status = 2;
+        /* raster: parallel over bands of window rows; key-min is order independent */
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int band = 0; band < (H + 7) / 8; ++band) {
+            int jb0 = band * 8, jb1 = jb0 + 7 < H - 1 ? jb0 + 7 : H - 1;
+            for (int j = jb0; j <= jb1; ++j)
+                for (int i = 0; i < W; ++i) { keys[(int64_t)j * W + i] = ~0ull; rbuf[(int64_t)j * W + i] = -1; }
+            for (int f = 0; f < F; ++f) {
+                for (int s = 0; s < nsub[f]; ++s) {
+                    int64_t ri = rec_index(F, f, s);
+                    const orc_rec *r = &recs[ri];
+                    if (!rec_nonempty(r)) continue;
+                    int j0 = r->j0 > jb0 ? r->j0 : jb0, j1 = r->j1 < jb1 ? r->j1 : jb1;
+                    for (int j = j0; j <= j1; ++j)
+                        for (int i = r->i0; i <= r->i1; ++i) {
+                            int64_t E[3];
+                            edge_values(r, i, j, E);
+                            if (!inside(r, E)) continue;
+                            uint32_t d;
+                            if (!sample_depth(r, i, j, &d)) continue;
+                            uint64_t key = ((uint64_t)d << 32) | (uint32_t)f;
+                            int64_t p = (int64_t)j * W + i;
+                            if (key < keys[p]) { keys[p] = key; rbuf[p] = (int32_t)ri; }
+                        }
+                }
+            }
+            /* resolve (R6) + background, rows flipped to top-first */
+            for (int j = jb0; j <= jb1; ++j) {
+                int row = H - 1 - j;
+                for (int i = 0; i < W; ++i) {
+                    int64_t p = (int64_t)j * W + i;
+                    int64_t o = (((int64_t)b * H + row) * W + i);
+                    float *out = pixels + o * C;
+                    const float *bg = background + o * C;
+                    int32_t ri = rbuf[p];
+                    if (gbuffer) gbuffer[o] = ri;
+                    if (ri < 0) {
+                        for (int c = 0; c < C; ++c) out[c] = bg[c];
+                        continue;
+                    }
+                    const orc_rec *r = &recs[ri];
+                    int64_t E[3];
+                    edge_values(r, i, j, E);
+                    float lam[3] = {0.0f, 0.0f, 0.0f};
+                    parent_lambda(r, E, lam);
+                    const int32_t *f3 = fb + 3 * (int64_t)r->face;
+                    for (int c = 0; c < C; ++c)
+                        out[c] = (lam[0] * cb[(int64_t)f3[0] * C + c] + lam[1] * cb[(int64_t)f3[1] * C + c]) +
+                                 lam[2] * cb[(int64_t)f3[2] * C + c];
+                }
+            }
+        }
+    }
+    free(recs); free(nsub); free(keys); free(rbuf);
+    return status;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Backward.  Contributions are computed in float exactly as the HIP kernel computes
+ * them; sums are accumulated in double (the GPU sums in float with atomics -> tolerance). */
+
+static int covers_face(const orc_rec *recs, const int32_t *nsub, int F, int f, int i, int j)
+{
+    for (int s = 0; s < nsub[f]; ++s) {
+        const orc_rec *r = &recs[rec_index(F, f, s)];
+        if (!rec_nonempty(r)) continue;
+        if (i < r->i0 || i > r->i1 || j < r->j0 || j > r->j1) continue;
+        int64_t E[3];
+        edge_values(r, i, j, E);
+        if (inside(r, E)) return 1;
+    }
+    return 0;
+}
+
+/* owner h (record r), pair midpoint between samples (i,j) and (i2,j2), axis 0=x 1=y */
+static void add_pair_owner(const orc_rec *r, const float *vb, const int32_t *fb, int W, int H,
+                           int i, int j, int i2, int j2, int axis, float s, float omega, double *gv)
+{
+    int64_t E1[3], E2[3], E[3];
+    edge_values(r, i, j, E1);
+    edge_values(r, i2, j2, E2);
+    for (int k = 0; k < 3; ++k) E[k] = E1[k] + E2[k];
+    float lam[3];
+    if (!parent_lambda(r, E, lam)) return;
+    const int32_t *f3 = fb + 3 * (int64_t)r->face;
+    float w0 = vb[(int64_t)f3[0] * 4 + 3], w1 = vb[(int64_t)f3[1] * 4 + 3], w2 = vb[(int64_t)f3[2] * 4 + 3];
+    float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
+    if (Wm == 0.0f) return;
+    float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
+    float mid = axis == 0 ? (float)(i + 1) : (float)(j + 1);
+    float ndc = mid / half - 1.0f;
+    float t = ((omega * s) * half) / Wm;
+    for (int k = 0; k < 3; ++k) {
+        float g = t * lam[k];
+        double *d = gv + (int64_t)f3[k] * 4;
+        d[axis] += (double)g;
+        d[3] += (double)(-(g * ndc));
+    }
+}
+
+int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces,
+                         const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
+                         int B, int H, int W, int C, int V, int F,
+                         float *grad_vertices, float *grad_vertex_colors, float *grad_background, int nthreads)
+{
+    (void)vertex_colors;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    int status = 0;
+    orc_rec *recs = (orc_rec *)malloc(sizeof(orc_rec) * 6 * (size_t)(F > 0 ? F : 1));
+    int32_t *nsub = (int32_t *)malloc(sizeof(int32_t) * (size_t)(F > 0 ? F : 1));
+    int nthr = 1;
+#ifdef _OPENMP
+    nthr = omp_get_max_threads();
+#endif
+    double *accv = (double *)malloc(sizeof(double) * (size_t)nthr * V * 4);
+    double *accc = (double *)malloc(sizeof(double) * (size_t)nthr * V * C);
+    for (int b = 0; b < B; ++b) {
+        const float *vb = vertices + (int64_t)b * V * 4;
+        const int32_t *fb = faces + (int64_t)b * F * 3;
+        if (setup_frame(vb, fb, V, F, W, H, recs, nsub)) status = 2;
+        memset(accv, 0, sizeof(double) * (size_t)nthr * V * 4);
+        memset(accc, 0, sizeof(double) * (size_t)nthr * V * C);
+#pragma omp parallel
+        {
+            int tid = 0;
+#ifdef _OPENMP
+            tid = omp_get_thread_num();
+#endif
+            double *gv = accv + (size_t)tid * V * 4, *gc = accc + (size_t)tid * V * C;
+#pragma omp for schedule(static)
+            for (int j = 0; j < H; ++j) {
+                for (int i = 0; i < W; ++i) {
+                    int row = H - 1 - j;
+                    int64_t o = ((int64_t)b * H + row) * W + i;
+                    const float *G = grad_pixels + o * C, *I = pixels + o * C;
+                    int32_t rp = gbuffer[o];
+                    float *gbg = grad_background + o * C;
+                    if (rp < 0) {
+                        for (int c = 0; c < C; ++c) gbg[c] = G[c];
+                    } else {
+                        for (int c = 0; c < C; ++c) gbg[c] = 0.0f;
+                        const orc_rec *r = &recs[rp];
+                        int64_t E[3];
+                        edge_values(r, i, j, E);
+                        float lam[3];
+                        if (parent_lambda(r, E, lam)) {
+                            const int32_t *f3 = fb + 3 * (int64_t)r->face;
+                            for (int k = 0; k < 3; ++k)
+                                for (int c = 0; c < C; ++c) gc[(int64_t)f3[k] * C + c] += (double)(lam[k] * G[c]);
+                        }
+                    }
+                    for (int axis = 0; axis < 2; ++axis) {
+                        int i2 = i + (axis == 0), j2 = j + (axis == 1);
+                        if (i2 >= W || j2 >= H) continue;
+                        int64_t o2 = ((int64_t)b * H + (H - 1 - j2)) * W + i2;
+                        int32_t rq = gbuffer[o2];
+                        if (rp < 0 && rq < 0) continue;
+                        const float *G2 = grad_pixels + o2 * C, *I2 = pixels + o2 * C;
+                        float acc = 0.0f;
+                        for (int c = 0; c < C; ++c) acc += (G[c] + G2[c]) * (I2[c] - I[c]);
+                        float s = -0.5f * acc;
+                        if (s == 0.0f) continue;
+                        int fp = rp >= 0 ? recs[rp].face : -1, fq = rq >= 0 ? recs[rq].face : -1;
+                        if (fp == fq || fq < 0) {
+                            add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                        } else if (fp < 0) {
+                            add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                        } else {
+                            int cfq = covers_face(recs, nsub, F, fp, i2, j2);
+                            int cgp = covers_face(recs, nsub, F, fq, i, j);
+                            if (!cfq && cgp) {
+                                add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                            } else if (cfq && !cgp) {
+                                add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                            } else {
+                                add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gv);
+                                add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gv);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        for (int64_t v = 0; v < (int64_t)V * 4; ++v) {
+            double a = 0.0;
+            for (int t = 0; t < nthr; ++t) a += accv[(size_t)t * V * 4 + v];
+            grad_vertices[(int64_t)b * V * 4 + v] = (float)a;
+        }
+        for (int64_t v = 0; v < (int64_t)V * C; ++v) {
+            double a = 0.0;
+            for (int t = 0; t < nthr; ++t) a += accc[(size_t)t * V * C + v];
+            grad_vertex_colors[(int64_t)b * V * C + v] = (float)a;
+        }
+    }
+    free(recs); free(nsub); free(accv); free(accc);
+    return status;
+}
+
+int oracle_max_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,179 @@
+"""Input generators for the parity tests and the bench (BASELINE.json configs).
+
+Each builder returns float32/int32 numpy arrays shaped like the reference op's inputs:
+background [H,W,C], vertices [V,4] (clip space), vertex_colors [V,C], faces [F,3].
+"""
+import math
+
+import numpy as np
+import torch
+
+from dirt_amd import lighting, matrices
+
+
+def readme_square(W=128, H=128, centre=(32.0, 64.0), size=16.0, C=1):
+    """README.md:27-70: a square of side `size` pixels centred at `centre` (window coords)."""
+    sq = np.array([[0, 0], [0, 1], [1, 1], [1, 0]], np.float32) * size - size / 2.0
+    sq = sq + np.array(centre, np.float32)
+    sq = sq * 2.0 / np.array([W, H], np.float32) - 1.0
+    v = np.concatenate([sq, np.zeros([4, 1], np.float32), np.ones([4, 1], np.float32)], 1).astype(np.float32)
+    return (np.zeros([H, W, C], np.float32), v, np.ones([4, C], np.float32), np.array([[0, 1, 2], [0, 2, 3]], np.int32))
+
+
+def _cube():
+    vertices = [[x, y, z] for z in [-1, 1] for y in [-1, 1] for x in [-1, 1]]
+    quads = [[0, 1, 3, 2], [4, 5, 7, 6], [1, 5, 4, 0], [2, 6, 7, 3], [4, 6, 2, 0], [3, 7, 5, 1]]
+    triangles = sum([[[a, b, c], [c, d, a]] for [a, b, c, d] in quads], [])
+    return np.array(vertices, np.float32), np.array(triangles, np.int32)
+
+
+def cube_scene(W=256, H=256, yaw=0.5):
+    """samples/simple.py:37-74 (Gouraud-lit, split-vertex cube; BASELINE config 2 at 256x256)."""
+    verts, faces = _cube()
+    verts, faces = lighting.split_vertices_by_face(torch.from_numpy(verts), torch.from_numpy(faces))
+    colors = torch.ones_like(verts)
+    verts_h = torch.cat([verts, torch.ones_like(verts[:, -1:])], 1)
+    world = verts_h @ matrices.rodrigues([0., yaw, 0.])
+    normals = lighting.vertex_normals_pre_split(world, faces)
+    view = matrices.compose(matrices.translation([0., -1.5, -3.5]), matrices.rodrigues([-0.3, 0., 0.]))
+    proj = matrices.perspective_projection(near=0.1, far=20., right=0.1, aspect=float(H) / W)
+    clip = world @ view @ proj
+    lit = lighting.diffuse_directional(normals, colors, light_direction=[1., 0., 0.], light_color=[1., 1., 1.]) * 0.8 \
+        + colors * 0.2
+    return (np.zeros([H, W, 3], np.float32), clip.numpy().astype(np.float32), lit.numpy().astype(np.float32),
+            faces.numpy().astype(np.int32))
+
+
+def make_cylinder(radius, height, end_offset, bevel, segments):
+    """tests/rasterise_tests.py:10-46 (Python-3 restatement)."""
+    angles = np.linspace(0., 2 * math.pi, segments, endpoint=False, dtype=np.float32)
+    xz = np.stack([np.cos(angles), np.sin(angles)], axis=1) * radius
+    top_bevel = np.stack([xz[:, 0] * (1. - bevel), np.ones(segments) * -height / 2. - radius * bevel, xz[:, 1] * (1. - bevel)], 1)
+    top = np.stack([xz[:, 0], np.ones(segments) * -height / 2., xz[:, 1]], 1)
+    bottom = np.stack([xz[:, 0], np.ones(segments) * height / 2., xz[:, 1]], 1)
+    bottom_bevel = np.stack([xz[:, 0] * (1. - bevel), np.ones(segments) * height / 2. + radius * bevel, xz[:, 1] * (1. - bevel)], 1)
+    ends = [[0., -height / 2. - end_offset, 0.], [0., height / 2. + end_offset, 0.]]
+    all_vertices = np.concatenate([top_bevel, top, bottom, bottom_bevel, ends], 0)
+    faces = []
+
+    def make_ring(start):
+        for q in range(segments):
+            uf, us = start + q, start + (q + 1) % segments
+            lf, ls = start + q + segments, start + (q + 1) % segments + segments
+            faces.extend([[uf, us, lf], [lf, us, ls]])
+    make_ring(0)
+    make_ring(segments)
+    make_ring(segments * 2)
+    for tf_ in range(segments):
+        ts = (tf_ + 1) % segments
+        bf = tf_ + segments * 3
+        bs = (bf + 1) % segments
+        faces.extend([[segments * 4, tf_, ts], [segments * 4 + 1, bf, bs]])
+    return all_vertices.astype(np.float32), np.array(faces, np.int32)
+
+
+def cylinder_clip_vertices(translation=(0., 0., -0.25), rotation_xy=0.0, W=48, H=36):
+    """Projected split cylinder of tests/rasterise_tests.py:49-77 as a function of the pose (torch, differentiable)."""
+    verts, faces = make_cylinder(0.2, 0.75, 0.1, 0., 10)
+    verts = np.concatenate([verts, np.ones([len(verts), 1], np.float32)], 1).astype(np.float32)
+    r = torch.as_tensor(rotation_xy, dtype=torch.float32)
+    t = torch.as_tensor(translation, dtype=torch.float32)
+    z, o = torch.zeros(()), torch.ones(())
+    view1 = torch.stack([
+        torch.stack([0.5 * torch.cos(r), 0.5 * -torch.sin(r), z, z]),
+        torch.stack([0.5 * torch.sin(r), 0.5 * torch.cos(r), z, z]),
+        torch.stack([z, z, 0.5 * o, z]),
+        torch.stack([z, z, z, o]),
+    ])
+    view2 = torch.stack([
+        torch.stack([o, z, z, z]), torch.stack([z, o, z, z]), torch.stack([z, z, o, z]),
+        torch.cat([t, o[None]]),
+    ])
+    sv, sf = lighting.split_vertices_by_face(torch.from_numpy(verts), torch.from_numpy(faces))
+    proj = matrices.perspective_projection(0.1, 20., 0.2, float(H) / W)
+    return sv @ view1 @ view2 @ proj, sf
+
+
+def cylinder_scene(W=48, H=36, seed=0, bgcolor=(0.4, 0.2, 0.2), vertex_color=(0.7, 0.3, 0.6)):
+    """tests/rasterise_tests.py:79-88: half-bgcolor background, first 75 vertices one colour."""
+    clip, faces = cylinder_clip_vertices((0., 0., -0.25), 0.0, W, H)
+    V = clip.shape[0]
+    rng = np.random.RandomState(seed)
+    cols = np.concatenate([np.tile(np.array(vertex_color, np.float32)[None], [75, 1]),
+                           rng.uniform(size=[V - 75, 3]).astype(np.float32)], 0)
+    bg = np.concatenate([np.tile(np.array(bgcolor, np.float32)[None, None], [H // 2, W, 1]),
+                         np.ones([H - H // 2, W, 3], np.float32)], 0)
+    return bg.astype(np.float32), clip.detach().numpy().astype(np.float32), cols, faces.numpy().astype(np.int32)
+
+
+def random_triangles(F=50000, W=1024, H=1024, C=3, radius_px=16.0, seed=0, perspective=False):
+    """SURVEY 8d synthetic distribution (BASELINE config 3): centres U[-1,1]^2, vertex offsets uniform in a
+    disk of radius `radius_px` pixels, z ~ U(-0.95,0.95) +-0.01 jitter, w=1 (or w~U(1,3) scaling xyz);
+    split vertices (V=3F), colours and background U[0,1]."""
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(-1, 1, size=(F, 1, 2))
+    ang = rng.uniform(0, 2 * np.pi, size=(F, 3))
+    rad = radius_px * np.sqrt(rng.uniform(0, 1, size=(F, 3)))
+    off = np.stack([np.cos(ang) * rad * 2.0 / W, np.sin(ang) * rad * 2.0 / H], -1)
+    xy = centres + off
+    z = rng.uniform(-0.95, 0.95, size=(F, 1)) + rng.uniform(-0.01, 0.01, size=(F, 3))
+    v = np.concatenate([xy, z[..., None], np.ones((F, 3, 1))], -1).reshape(F * 3, 4)
+    if perspective:
+        w = rng.uniform(1, 3, size=(F * 3, 1))
+        v = v * w
+    faces = np.arange(3 * F, dtype=np.int32).reshape(F, 3)
+    cols = rng.uniform(0, 1, size=(3 * F, C))
+    bg = rng.uniform(0, 1, size=(H, W, C))
+    return bg.astype(np.float32), v.astype(np.float32), cols.astype(np.float32), faces
+
+
+def clipping_scene(W=96, H=64, C=3, seed=3):
+    """Triangles crossing the near plane, behind the camera, and far outside the guard band (R5)."""
+    rng = np.random.default_rng(seed)
+    tris = []
+    for _ in range(40):
+        p = rng.uniform(-3, 3, size=(3, 3))
+        w = rng.uniform(-0.6, 2.0, size=(3, 1))
+        z = rng.uniform(-1.5, 1.5, size=(3, 1)) * np.abs(w)
+        tris.append(np.concatenate([p[:, :2], z, w], 1))
+    # huge triangle spanning far beyond the guard band, fully in front
+    tris.append(np.array([[-5000, -5000, 0.1, 1], [5000, -5000, 0.1, 1], [0, 8000, 0.1, 1]], np.float64))
+    # triangle with one vertex behind the eye
+    tris.append(np.array([[-0.5, -0.5, 0.2, 1], [0.5, -0.5, 0.2, 1], [0.0, 0.6, -0.5, -0.3]], np.float64))
+    v = np.concatenate(tris, 0).astype(np.float32)
+    F = len(tris)
+    faces = np.arange(3 * F, dtype=np.int32).reshape(F, 3)
+    cols = rng.uniform(0, 1, size=(3 * F, C)).astype(np.float32)
+    bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
+    return bg, v, cols, faces
+
+
+def shared_mesh_scene(W=80, H=60, C=3, seed=5, n=12):
+    """A jittered grid mesh with SHARED vertices (non-split), partly occluding a second grid."""
+    rng = np.random.default_rng(seed)
+    verts, faces = [], []
+    for layer, z in enumerate([0.2, -0.1]):
+        base = len(verts)
+        xs = np.linspace(-0.9 + 0.3 * layer, 0.6 + 0.3 * layer, n)
+        ys = np.linspace(-0.8, 0.8 - 0.3 * layer, n)
+        for yy in ys:
+            for xx in xs:
+                verts.append([xx + rng.uniform(-0.02, 0.02), yy + rng.uniform(-0.02, 0.02), z + rng.uniform(-0.05, 0.05), 1.0])
+        for r in range(n - 1):
+            for c in range(n - 1):
+                a = base + r * n + c
+                faces.append([a, a + 1, a + n])
+                faces.append([a + 1, a + n + 1, a + n])
+    v = np.array(verts, np.float32)
+    f = np.array(faces, np.int32)
+    cols = rng.uniform(0, 1, size=(len(v), C)).astype(np.float32)
+    bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
+    return bg, v, cols, f
+
+
+def batch_of(scene_fn, B, **kw):
+    """Stack B independent frames of a scene builder (seed offset by frame index)."""
+    seed0 = kw.pop("seed", 0)
+    takes_seed = "seed" in scene_fn.__code__.co_varnames
+    frames = [scene_fn(seed=seed0 + b, **kw) if takes_seed else scene_fn(**kw) for b in range(B)]
+    return tuple(np.stack([fr[k] for fr in frames]) for k in range(4))
