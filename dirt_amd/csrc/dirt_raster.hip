@@ -450,7 +450,16 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 }
 
 // ------------------------------------------------------------------------------------------------
-// K5: backward (first version: per-pixel contributions, global float atomics)
+// K5: backward
+//
+// One 256-thread workgroup per 16x16 tile, one lane per pixel.  Every contribution of a lane goes to
+// the face visible at its own pixel: colour gradients lambda_k * G, and the share of the four
+// neighbour pairs around the pixel that this face owns (a pair's other owner is handled by the lane
+// on the other side, same-face pairs by the lower lane only).  Reduction without global contention:
+//   1. DPP segmented scan along each 16-pixel row (one DPP row == one pixel row) sums runs of equal
+//      record index into the run's last lane;
+//   2. run tails ds_add into a per-tile LDS hash table keyed by record index;
+//   3. one wave-instruction of global float atomics per (tile, record): <= 9+3C lanes, ~3 cache lines.
 
 __device__ bool covers_face(const Rec *frame_recs, const int32_t *nsub_frame, int F, int f, int i, int j)
 {
@@ -465,97 +474,208 @@ __device__ bool covers_face(const Rec *frame_recs, const int32_t *nsub_frame, in
     return false;
 }
 
-__device__ void add_pair_owner(const Rec &r, const float *vb, const int32_t *fb, int W, int H, int i, int j, int i2,
-                               int j2, int axis, float s, float omega, float *gvb)
+template <int D>
+__device__ __forceinline__ float dpp_shr_f(float v)  // lane l <- lane l-D of the same 16-lane row, 0 if none
 {
-    int64_t E1[3], E2[3], E[3];
-    edge_values(r, i, j, E1);
-    edge_values(r, i2, j2, E2);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) E[k] = E1[k] + E2[k];
-    float lam[3];
-    if (!parent_lambda(r, E, lam)) return;
-    const int32_t *f3 = fb + 3 * (int64_t)r.face;
-    const float w0 = vb[(int64_t)f3[0] * 4 + 3], w1 = vb[(int64_t)f3[1] * 4 + 3], w2 = vb[(int64_t)f3[2] * 4 + 3];
-    const float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
-    if (Wm == 0.0f) return;
-    const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
-    const float mid = axis == 0 ? (float)(i + 1) : (float)(j + 1);
-    const float ndc = mid / half - 1.0f;
-    const float tt = ((omega * s) * half) / Wm;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float g = tt * lam[k];
-        float *d = gvb + (int64_t)f3[k] * 4;
-        atomicAdd(d + axis, g);
-        atomicAdd(d + 3, -(g * ndc));
-    }
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x110 + D, 0xF, 0xF, false));
+}
+template <int D>
+__device__ __forceinline__ int dpp_shr_i(int v, int fill)
+{
+    return __builtin_amdgcn_update_dpp(fill, v, 0x110 + D, 0xF, 0xF, false);
+}
+template <int D>
+__device__ __forceinline__ int dpp_shl_i(int v, int fill)  // lane l <- lane l+D of the same row
+{
+    return __builtin_amdgcn_update_dpp(fill, v, 0x100 + D, 0xF, 0xF, false);
 }
 
+constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
+constexpr int kHashSlots = 256;    // >= distinct records a 256-pixel tile can hold
+
+template <int CC>
 __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ verts, const int32_t *__restrict__ faces,
                                                    const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
-                                                   const int32_t *__restrict__ nsub, int B, int H, int W, int C, int V,
-                                                   int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
+                                                   const int32_t *__restrict__ nsub, int B, int H, int W, int Cdyn,
+                                                   int V, int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
                                                    float *__restrict__ grad_colors, float *__restrict__ grad_bg)
 {
+    constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
+    constexpr int NVM = 9 + 3 * CM;
+    const int C = CC > 0 ? CC : Cdyn;
+    const int NV = 9 + 3 * C;
+    __shared__ int32_t s_rec[kHalo * kHalo];
+    __shared__ float s_G[kHalo * kHalo * CM];
+    __shared__ float s_I[kHalo * kHalo * CM];
+    __shared__ int32_t s_keys[kHashSlots];
+    __shared__ int32_t s_list[kHashSlots];
+    __shared__ float s_vals[kHashSlots * NVM];
+    __shared__ int32_t s_n;
+
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
-    const int t = threadIdx.x;
-    const int i = tx * kTile + (t & 15), j = ty * kTile + (t >> 4);
-    if (i >= W || j >= H) return;
+    const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
+    const int i = tx * kTile + lx, j = ty * kTile + ly;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const int32_t *nsub_frame = nsub + (int64_t)b * F;
     const float *vb = verts + (int64_t)b * V * 4;
     const int32_t *fb = faces + (int64_t)b * F * 3;
-    float *gvb = grad_verts + (int64_t)b * V * 4;
-    float *gcb = grad_colors + (int64_t)b * V * C;
-    const int row = H - 1 - j;
-    const int64_t o = ((int64_t)b * H + row) * W + i;
-    const float *G = grad_pixels + o * C, *I = pixels + o * C;
-    const int32_t rp = gbuffer[o];
-    float *gbg = grad_bg + o * C;
-    if (rp < 0) {
-        for (int c = 0; c < C; ++c) gbg[c] = G[c];
-    } else {
-        for (int c = 0; c < C; ++c) gbg[c] = 0.0f;
-        const Rec &r = frame_recs[rp];
-        int64_t E[3];
-        edge_values(r, i, j, E);
-        float lam[3];
-        if (parent_lambda(r, E, lam)) {
-            const int32_t *f3 = fb + 3 * (int64_t)r.face;
-            for (int k = 0; k < 3; ++k)
-                for (int c = 0; c < C; ++c) atomicAdd(gcb + (int64_t)f3[k] * C + c, lam[k] * G[c]);
+
+    for (int k = t; k < kHashSlots; k += 256) s_keys[k] = -1;
+    for (int k = t; k < kHashSlots * NVM; k += 256) s_vals[k] = 0.0f;
+    if (t == 0) s_n = 0;
+    // stage gbuffer / G / I of the tile plus a one-pixel halo (window coords, j from the bottom)
+    const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
+    for (int k = t; k < kHalo * kHalo; k += 256) {
+        const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
+        if (hi < 0 || hj < 0 || hi >= W || hj >= H) {
+            s_rec[k] = -2;
+            continue;
+        }
+        const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
+        s_rec[k] = gbuffer[o];
+        for (int c = 0; c < C; ++c) {
+            s_G[k * CM + c] = grad_pixels[o * C + c];
+            s_I[k * CM + c] = pixels[o * C + c];
         }
     }
-    for (int axis = 0; axis < 2; ++axis) {
-        const int i2 = i + (axis == 0), j2 = j + (axis == 1);
-        if (i2 >= W || j2 >= H) continue;
-        const int64_t o2 = ((int64_t)b * H + (H - 1 - j2)) * W + i2;
-        const int32_t rq = gbuffer[o2];
-        if (rp < 0 && rq < 0) continue;
-        const float *G2 = grad_pixels + o2 * C, *I2 = pixels + o2 * C;
-        float acc = 0.0f;
-        for (int c = 0; c < C; ++c) acc += (G[c] + G2[c]) * (I2[c] - I[c]);
-        const float s = -0.5f * acc;
-        if (s == 0.0f) continue;
-        const int fp = rp >= 0 ? frame_recs[rp].face : -1, fq = rq >= 0 ? frame_recs[rq].face : -1;
-        if (fp == fq || fq < 0) {
-            add_pair_owner(frame_recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
-        } else if (fp < 0) {
-            add_pair_owner(frame_recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
-        } else {
-            const bool cfq = covers_face(frame_recs, nsub_frame, F, fp, i2, j2);
-            const bool cgp = covers_face(frame_recs, nsub_frame, F, fq, i, j);
-            if (!cfq && cgp) {
-                add_pair_owner(frame_recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
-            } else if (cfq && !cgp) {
-                add_pair_owner(frame_recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gvb);
-            } else {
-                add_pair_owner(frame_recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gvb);
-                add_pair_owner(frame_recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gvb);
+    __syncthreads();
+
+    const bool in_frame = i < W && j < H;
+    const int kme = (ly + 1) * kHalo + (lx + 1);
+    const int32_t rp = in_frame ? s_rec[kme] : -2;
+    if (in_frame) {
+        const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
+        for (int c = 0; c < C; ++c) grad_bg[o * C + c] = rp < 0 ? s_G[kme * CM + c] : 0.0f;
+    }
+
+    float acc[NVM];
+#pragma unroll
+    for (int v = 0; v < NVM; ++v) acc[v] = 0.0f;
+    int key = -1;
+    if (rp >= 0) {
+        const Rec r = frame_recs[rp];
+        const int f = r.face;
+        const int32_t *f3 = fb + 3 * (int64_t)f;
+        const int v0 = f3[0], v1 = f3[1], v2 = f3[2];
+        const float w0 = vb[(int64_t)v0 * 4 + 3], w1 = vb[(int64_t)v1 * 4 + 3], w2 = vb[(int64_t)v2 * 4 + 3];
+        int64_t Ep[3];
+        edge_values(r, i, j, Ep);
+        {
+            float lam[3];
+            if (parent_lambda(r, Ep, lam)) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * s_G[kme * CM + c];
             }
+        }
+        // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window)
+#pragma unroll
+        for (int dir = 0; dir < 4; ++dir) {
+            const int axis = dir >> 1;
+            const bool me_low = (dir & 1) == 0;
+            const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
+            const int kq = kme + dj * kHalo + di;
+            const int32_t rq = s_rec[kq];
+            if (rq == -2) continue;
+            const int klo = me_low ? kme : kq, kup = me_low ? kq : kme;
+            float a = 0.0f;
+            for (int c = 0; c < C; ++c)
+                a += (s_G[klo * CM + c] + s_G[kup * CM + c]) * (s_I[kup * CM + c] - s_I[klo * CM + c]);
+            const float s = -0.5f * a;
+            if (s == 0.0f) continue;
+            const int iq = i + di, jq = j + dj;
+            const int fq = rq >= 0 ? frame_recs[rq].face : -1;
+            float omega;
+            if (fq == f) {
+                omega = me_low ? 1.0f : 0.0f;
+            } else if (fq < 0) {
+                omega = 1.0f;
+            } else {
+                const bool mine_covers_other = covers_face(frame_recs, nsub_frame, F, f, iq, jq);
+                const bool other_covers_me = covers_face(frame_recs, nsub_frame, F, fq, i, j);
+                omega = (!mine_covers_other && other_covers_me) ? 1.0f
+                        : (mine_covers_other && !other_covers_me) ? 0.0f : 0.5f;
+            }
+            if (omega == 0.0f) continue;
+            int64_t Eq[3], E[3];
+            edge_values(r, iq, jq, Eq);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) E[k] = Ep[k] + Eq[k];
+            float lam[3];
+            if (!parent_lambda(r, E, lam)) continue;
+            const float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
+            if (Wm == 0.0f) continue;
+            const int ilo = me_low ? i : iq, jlo = me_low ? j : jq;
+            const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
+            const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
+            const float ndc = mid / half - 1.0f;
+            const float tt = ((omega * s) * half) / Wm;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float g = tt * lam[k];
+                acc[k * 3 + axis] += g;
+                acc[k * 3 + 2] += -(g * ndc);
+            }
+        }
+        key = rp;
+    }
+
+    // 1. segmented sum over runs of equal key along the 16-lane row
+    const int kl = dpp_shr_i<1>(key, -3);
+    int start = (lx == 0 || kl != key) ? lx : -1;
+    start = max(start, dpp_shr_i<1>(start, -1));
+    start = max(start, dpp_shr_i<2>(start, -1));
+    start = max(start, dpp_shr_i<4>(start, -1));
+    start = max(start, dpp_shr_i<8>(start, -1));
+#pragma unroll
+    for (int v = 0; v < NVM; ++v) {
+        float x = acc[v];
+        float y;
+        y = dpp_shr_f<1>(x); if (lx - 1 >= start) x += y;
+        y = dpp_shr_f<2>(x); if (lx - 2 >= start) x += y;
+        y = dpp_shr_f<4>(x); if (lx - 4 >= start) x += y;
+        y = dpp_shr_f<8>(x); if (lx - 8 >= start) x += y;
+        acc[v] = x;
+    }
+    const int kr = dpp_shl_i<1>(key, -3);
+    const bool tail = key >= 0 && (lx == 15 || kr != key);
+
+    // 2. run tails accumulate into the tile's LDS hash table
+    if (tail) {
+        int slot = (int)(((uint32_t)key * 2654435761u) >> 24) & (kHashSlots - 1);
+        while (true) {
+            const int old = atomicCAS(&s_keys[slot], -1, key);
+            if (old == -1) {
+                s_list[atomicAdd(&s_n, 1)] = slot;
+                break;
+            }
+            if (old == key) break;
+            slot = (slot + 1) & (kHashSlots - 1);
+        }
+        for (int v = 0; v < NV; ++v)
+            if (acc[v] != 0.0f) atomicAdd(&s_vals[slot * NVM + v], acc[v]);
+    }
+    __syncthreads();
+
+    // 3. flush: one wave-instruction of global atomics per (tile, record)
+    const int n = s_n, wave = t >> 6, lane = t & 63;
+    float *gvb = grad_verts + (int64_t)b * V * 4;
+    float *gcb = grad_colors + (int64_t)b * V * C;
+    for (int e = wave; e < n; e += 4) {
+        const int slot = s_list[e];
+        if (lane >= NV) continue;
+        const float val = s_vals[slot * NVM + lane];
+        if (val == 0.0f) continue;
+        const int f = frame_recs[s_keys[slot]].face;
+        const int32_t *f3 = fb + 3 * (int64_t)f;
+        if (lane < 9) {
+            const int k = lane / 3, comp = lane % 3;
+            atomicAdd(gvb + (int64_t)f3[k] * 4 + (comp == 2 ? 3 : comp), val);
+        } else {
+            const int k = (lane - 9) / C, c = (lane - 9) % C;
+            atomicAdd(gcb + (int64_t)f3[k] * C + c, val);
         }
     }
 }
@@ -678,9 +798,14 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_GRAD, stream);
-    grad_kernel<<<grid, dim3(256), 0, stream>>>(vertices, faces, pixels, grad_pixels, gbuffer, recs, nsub, B, H, W, C,
-                                                V, F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,
-                                                grad_background);
+#define LAUNCH_GRAD(CC)                                                                                      \
+    grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(vertices, faces, pixels, grad_pixels, gbuffer, recs, nsub, B, H, \
+                                                    W, C, V, F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,   \
+                                                    grad_background)
+    if (C == 1) LAUNCH_GRAD(1);
+    else if (C == 3) LAUNCH_GRAD(3);
+    else LAUNCH_GRAD(0);
+#undef LAUNCH_GRAD
     HIP_TRY(hipGetLastError());
     return DIRT_OK;
 }
