@@ -5,15 +5,16 @@
 //
 //   K1 setup_kernel    one thread per (frame, face): fetch 3 clip vertices, project + snap (R1/R2),
 //                      edge equations (R3), depth plane (R4), guard-band clipping (R5, rare slow path);
-//                      writes 128-B setup records and counts (tile, triangle) bin entries.
+//                      writes 128-B setup records + 32-B FaceData, counts (tile, triangle) bin entries.
 //   K2 scan_kernel     exclusive scan of per-tile counts.
 //   K3 fill_kernel     scatter each record index into the bins of the 16x16 tiles its bbox overlaps.
-//   K4 raster_kernel   one 256-thread workgroup per 16x16 tile: stages the tile's records in LDS,
-//                      each lane owns one pixel and keeps the min (depth24<<32 | face) key, then
-//                      resolves in-kernel: perspective-correct Gouraud colour (R6) or background,
-//                      coalesced [B,H,W,C] writes + the int32 g-buffer.  This fuses the reference's
+//   K4 raster_kernel   one 256-thread workgroup per 16x16 tile (a wave per 16x4 strip): stages the
+//                      tile's records in LDS with strip-relative 32-bit edge values (exact), each lane
+//                      owns one pixel and keeps the min (depth24<<32 | face) key, then resolves
+//                      in-kernel: perspective-correct Gouraud colour (R6) or background, coalesced
+//                      [B,H,W,C] writes + the int32 g-buffer.  This fuses the reference's
 //                      upload_background + raster + second pass + download_pixels
-//                      (csrc/rasterise_egl.cu:16-129, rasterise_egl.cpp:370-503) into one pass over HBM.
+//                      (csrc/rasterise_egl.cu:16-129, rasterise_egl.cpp:370-503) into one HBM pass.
 //   K5 grad_kernel     backward: dL/dbackground, dL/dvertex_colors and the
 //                      filter-based dL/dvertices (README.md:146-147) for the gradient contract of
 //                      csrc/rasterise_grad_common.h:19-24.
@@ -34,6 +35,22 @@ using namespace dirt;
 namespace {
 
 thread_local std::string g_last_error;
+
+int fail(int code, const char *msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess) {                                                         \
+            char _b[256];                                                               \
+            snprintf(_b, sizeof(_b), "%s failed: %s", #expr, hipGetErrorString(_e));    \
+            return fail(DIRT_EHIP, _b);                                                 \
+        }                                                                               \
+    } while (0)
 
 // ------------------------------------------------------------------------------------------------
 // Optional per-kernel event timing (bench.py roofline); off by default, host-side only.
@@ -63,32 +80,16 @@ struct ProfScope {
     }
 };
 
-int fail(int code, const char *msg)
-{
-    g_last_error = msg;
-    return code;
-}
-
-#define HIP_TRY(expr)                                                                   \
-    do {                                                                                \
-        hipError_t _e = (expr);                                                         \
-        if (_e != hipSuccess) {                                                         \
-            char _b[256];                                                               \
-            snprintf(_b, sizeof(_b), "%s failed: %s", #expr, hipGetErrorString(_e));    \
-            return fail(DIRT_EHIP, _b);                                                 \
-        }                                                                               \
-    } while (0)
-
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
 // ------------------------------------------------------------------------------------------------
-// Workspace layout
+// Workspace layout.  saved = records [B][6F] (128 B) + FaceData [B][F] (32 B): what the backward reads.
+// scratch = per-tile counts, cursors, offsets and the bins (forward only).
 struct Layout {
-    int ntx, nty, ntiles;       // tiles per frame
-    int64_t nrec;               // records per frame = 6F
-    size_t saved_recs, saved_nsub, saved_total;
-    size_t off_count, off_cursor, off_offset, off_scan_tmp, off_flag, off_bins, scratch_total;
-    size_t scan_tmp_bytes;
+    int ntx, nty, ntiles;
+    int64_t nrec;
+    size_t saved_recs, saved_fdata, saved_total;
+    size_t off_count, off_cursor, off_offset, off_flag, off_bins, scratch_total;
     int64_t bin_capacity;
 };
 
@@ -109,17 +110,14 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.bin_capacity = bin_capacity > 0 ? (bin_capacity > 0x7fffffffLL ? 0x7fffffffLL : bin_capacity)
                                       : default_capacity(B, F, L.ntiles);
     L.saved_recs = 0;
-    L.saved_nsub = (size_t)align_up((int64_t)B * L.nrec * (int64_t)sizeof(Rec), 256);
-    L.saved_total = L.saved_nsub + (size_t)align_up((int64_t)B * F * 4, 256);
+    L.saved_fdata = (size_t)align_up((int64_t)B * L.nrec * (int64_t)sizeof(Rec), 256);
+    L.saved_total = L.saved_fdata + (size_t)align_up((int64_t)B * F * (int64_t)sizeof(FaceData), 256);
     const int64_t nt = (int64_t)B * L.ntiles;
-    const size_t tmp = 0;
-    L.scan_tmp_bytes = tmp;
     size_t o = 0;
     L.off_count = o;  o += (size_t)align_up(nt * 4, 256);
     L.off_cursor = o; o += (size_t)align_up(nt * 4, 256);
     L.off_offset = o; o += (size_t)align_up(nt * 8, 256);
     L.off_flag = o;   o += 256;
-    L.off_scan_tmp = o; o += (size_t)align_up((int64_t)tmp, 256);
     L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 4, 256);
     L.scratch_total = o;
     return DIRT_OK;
@@ -155,14 +153,15 @@ __device__ inline float plane_dist(int p, const float *v, float gx, float gy)
     }
 }
 
-// R5 slow path: clip against z>=-w and the guard planes, fan-triangulate. Returns nsub.
-__device__ __noinline__ int clip_face(const float (*v)[4], int W, int H, int F, int f, Rec *frame_recs)
+// R5 slow path: clip against z>=-w and the guard planes, fan-triangulate, write the sub-records.
+// Not inlined so that its stack arrays do not inflate the fast path.  Returns nsub.
+__device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *frame_recs)
 {
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
     float poly[9][7], tmp[9][7];
     int n = 3;
     for (int k = 0; k < 3; ++k) {
-        for (int c = 0; c < 4; ++c) poly[k][c] = v[k][c];
+        for (int c = 0; c < 4; ++c) poly[k][c] = tri.v[k][c];
         for (int i = 0; i < 3; ++i) poly[k][4 + i] = (i == k) ? 1.0f : 0.0f;
     }
     for (int p = 0; p < 5; ++p) {
@@ -197,72 +196,87 @@ __device__ __noinline__ int clip_face(const float (*v)[4], int W, int H, int F, 
             for (int c = 0; c < 4; ++c) sv[k][c] = poly[idx[k]][c];
             for (int i = 0; i < 3; ++i) sb[k][i] = poly[idx[k]][4 + i];
         }
-        make_record(sv, sb, W, H, f, &frame_recs[rec_index(F, f, s)]);
+        Rec r;
+        make_record(sv, sb, W, H, f, r);
+        frame_recs[rec_index(F, f, s)] = r;
     }
     return nsub;
 }
 
-__device__ inline void count_tiles(const Rec &r, int ntx, uint32_t *tile_count_frame)
+__device__ inline void count_tiles(int i0, int i1, int j0, int j1, int ntx, uint32_t *tile_count_frame)
 {
-    if (r.i0 > r.i1) return;
-    const int tx0 = r.i0 / kTile, tx1 = r.i1 / kTile, ty0 = r.j0 / kTile, ty1 = r.j1 / kTile;
+    if (i0 > i1) return;
+    const int tx0 = i0 / kTile, tx1 = i1 / kTile, ty0 = j0 / kTile, ty1 = j1 / kTile;
     for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&tile_count_frame[ty * ntx + tx], 1u);
 }
 
-__global__ __launch_bounds__(256) void setup_kernel(const float *__restrict__ verts, const int32_t *__restrict__ faces,
-                                                    int B, int V, int F, int W, int H, int ntx, int ntiles, int64_t nrec,
-                                                    Rec *__restrict__ recs, int32_t *__restrict__ nsub,
-                                                    uint32_t *__restrict__ tile_count, uint32_t *__restrict__ flag)
+constexpr int kSetupThreads = 64;  // 50k faces -> 784 workgroups: spread over all 256 CUs
+
+__global__ __launch_bounds__(kSetupThreads) void setup_kernel(const float *__restrict__ verts,
+                                                              const int32_t *__restrict__ faces, int B, int V, int F,
+                                                              int W, int H, int ntx, int ntiles, int64_t nrec,
+                                                              Rec *__restrict__ recs, FaceData *__restrict__ fdata,
+                                                              uint32_t *__restrict__ tile_count, uint32_t *__restrict__ flag)
 {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (int64_t)B * F) return;
     const int b = (int)(gid / F), f = (int)(gid - (int64_t)b * F);
     Rec *frame_recs = recs + (int64_t)b * nrec;
-    const int32_t *f3 = faces + gid * 3;
     const float *vb = verts + (int64_t)b * V * 4;
-    float v[3][4];
+    const int32_t i0 = faces[gid * 3], i1 = faces[gid * 3 + 1], i2 = faces[gid * 3 + 2];
+    const int32_t vidx[3] = {i0, i1, i2};
+    Tri tri;
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const int32_t vi = f3[k];
+        const int32_t vi = vidx[k];
         if (vi < 0 || vi >= V) {
             ok = false;
-            atomicOr(flag, 1u);
-            v[k][0] = v[k][1] = v[k][2] = 0.0f; v[k][3] = 1.0f;
+            tri.v[k][0] = tri.v[k][1] = tri.v[k][2] = 0.0f;
+            tri.v[k][3] = 1.0f;
         } else {
             const float4 p = *reinterpret_cast<const float4 *>(vb + (int64_t)vi * 4);
-            v[k][0] = p.x; v[k][1] = p.y; v[k][2] = p.z; v[k][3] = p.w;
-            ok = ok && finite4(v[k]);
+            tri.v[k][0] = p.x; tri.v[k][1] = p.y; tri.v[k][2] = p.z; tri.v[k][3] = p.w;
+            ok = ok && finite4(tri.v[k]);
         }
     }
+    if (!(i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V)) atomicOr(flag, 1u);
     uint32_t *tc = tile_count + (int64_t)b * ntiles;
-    Rec &r0 = frame_recs[f];
-    if (!ok) {
-        set_empty(&r0, f);
-        nsub[gid] = 0;
-        return;
-    }
-    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
-    bool fast = true;
+    FaceData fd;
+    fd.v[0] = i0; fd.v[1] = i1; fd.v[2] = i2;
+    fd.w[0] = tri.v[0][3]; fd.w[1] = tri.v[1][3]; fd.w[2] = tri.v[2][3];
+    fd.pad = 0;
+    Rec r;
+    set_empty(r, f);
+    int nsub = 0;
+    if (ok) {
+        const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+        bool fast = true;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float w = v[k][3];
-        fast = fast && (w > 0.0f && fabsf(v[k][0]) <= gx * w && fabsf(v[k][1]) <= gy * w);
+        for (int k = 0; k < 3; ++k) {
+            const float w = tri.v[k][3];
+            fast = fast && (w > 0.0f && fabsf(tri.v[k][0]) <= gx * w && fabsf(tri.v[k][1]) <= gy * w);
+        }
+        if (fast) {
+            const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
+            make_record(tri.v, id, W, H, f, r);
+            nsub = 1;
+            frame_recs[f] = r;
+            count_tiles(r.i0, r.i1, r.j0, r.j1, ntx, tc);
+        } else {
+            frame_recs[f] = r;  // empty unless clip_face overwrites it
+            nsub = clip_face(tri, W, H, F, f, frame_recs);
+            for (int s = 0; s < nsub; ++s) {
+                const Rec &q = frame_recs[rec_index(F, f, s)];
+                count_tiles(q.i0, q.i1, q.j0, q.j1, ntx, tc);
+            }
+        }
+    } else {
+        frame_recs[f] = r;
     }
-    if (fast) {
-        const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
-        Rec r;
-        make_record(v, id, W, H, f, &r);
-        r0 = r;
-        nsub[gid] = 1;
-        count_tiles(r, ntx, tc);
-        return;
-    }
-    set_empty(&r0, f);
-    const int n = clip_face(v, W, H, F, f, frame_recs);
-    nsub[gid] = n;
-    for (int s = 0; s < n; ++s) count_tiles(frame_recs[rec_index(F, f, s)], ntx, tc);
+    fd.nsub = nsub;
+    fdata[gid] = fd;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -282,12 +296,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__re
         const int64_t k0 = base + (int64_t)t * kScanPerThread;
         uint32_t v[kScanPerThread];
         uint64_t local = 0;
+        if (k0 + kScanPerThread <= n) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(in + k0);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
 #pragma unroll
-        for (int q = 0; q < kScanPerThread; ++q) {
-            v[q] = (k0 + q < n) ? in[k0 + q] : 0u;
-            local += v[q];
+            for (int q = 0; q < kScanPerThread; ++q) v[q] = (k0 + q < n) ? in[k0 + q] : 0u;
         }
-        // inclusive wave scan of the per-thread sums
+#pragma unroll
+        for (int q = 0; q < kScanPerThread; ++q) local += v[q];
         uint64_t x = local;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -303,7 +320,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__re
                 const uint64_t y = __shfl_up(w, d, 64);
                 if (lane >= d) w += y;
             }
-            if (lane < kScanThreads / 64) wave_sums[lane] = w;  // inclusive
+            if (lane < kScanThreads / 64) wave_sums[lane] = w;
             if (lane == kScanThreads / 64 - 1) carry_s = w;
         }
         __syncthreads();
@@ -319,59 +336,155 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__re
 }
 
 // ------------------------------------------------------------------------------------------------
-// K3: fill bins (order inside a bin is irrelevant: the depth resolve is a commutative min)
+// K3: fill bins (order inside a bin is irrelevant: the depth resolve is a commutative min).
+// The common <= 3x3-tile case issues all its returning atomics back to back (one latency, not n).
 
-__global__ __launch_bounds__(256) void fill_kernel(const Rec *__restrict__ recs, const int32_t *__restrict__ nsub,
-                                                   int B, int F, int ntx, int ntiles, int64_t nrec,
-                                                   const uint64_t *__restrict__ tile_offset,
-                                                   uint32_t *__restrict__ tile_cursor, int32_t *__restrict__ bins,
-                                                   int64_t capacity)
+__device__ inline void fill_one(int64_t ri, int i0, int i1, int j0, int j1, int b, int ntx, int ntiles,
+                                const uint64_t *__restrict__ tile_offset, uint32_t *__restrict__ tile_cursor,
+                                int32_t *__restrict__ bins, int64_t capacity)
+{
+    if (i0 > i1) return;
+    const int tx0 = i0 / kTile, tx1 = i1 / kTile, ty0 = j0 / kTile, ty1 = j1 / kTile;
+    const int nx = tx1 - tx0 + 1, ny = ty1 - ty0 + 1;
+    const int64_t base = (int64_t)b * ntiles;
+    if (nx <= 3 && ny <= 3) {
+        uint32_t pos[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const int qx = q % 3, qy = q / 3;
+            if (qx < nx && qy < ny) pos[q] = atomicAdd(&tile_cursor[base + (ty0 + qy) * ntx + tx0 + qx], 1u);
+        }
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const int qx = q % 3, qy = q / 3;
+            if (qx < nx && qy < ny) {
+                const int64_t t = base + (ty0 + qy) * ntx + tx0 + qx;
+                const uint64_t dst = tile_offset[t] + pos[q];
+                if (dst < (uint64_t)capacity) bins[dst] = (int32_t)ri;
+            }
+        }
+        return;
+    }
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+            const int64_t t = base + ty * ntx + tx;
+            const uint32_t pos = atomicAdd(&tile_cursor[t], 1u);
+            const uint64_t dst = tile_offset[t] + pos;
+            if (dst < (uint64_t)capacity) bins[dst] = (int32_t)ri;
+        }
+}
+
+__global__ __launch_bounds__(kSetupThreads) void fill_kernel(const Rec *__restrict__ recs,
+                                                             const FaceData *__restrict__ fdata, int B, int F, int ntx,
+                                                             int ntiles, int64_t nrec,
+                                                             const uint64_t *__restrict__ tile_offset,
+                                                             uint32_t *__restrict__ tile_cursor,
+                                                             int32_t *__restrict__ bins, int64_t capacity)
 {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (int64_t)B * F) return;
     const int b = (int)(gid / F), f = (int)(gid - (int64_t)b * F);
-    const int n = nsub[gid];
+    const Rec *frame_recs = recs + (int64_t)b * nrec;
+    const int n = fdata[gid].nsub;
     for (int s = 0; s < n; ++s) {
         const int64_t ri = rec_index(F, f, s);
-        const Rec &r = recs[(int64_t)b * nrec + ri];
-        if (r.i0 > r.i1) continue;
-        const int tx0 = r.i0 / kTile, tx1 = r.i1 / kTile, ty0 = r.j0 / kTile, ty1 = r.j1 / kTile;
-        for (int ty = ty0; ty <= ty1; ++ty)
-            for (int tx = tx0; tx <= tx1; ++tx) {
-                const int64_t t = (int64_t)b * ntiles + ty * ntx + tx;
-                const uint32_t pos = atomicAdd(&tile_cursor[t], 1u);
-                const uint64_t dst = tile_offset[t] + pos;
-                if (dst < (uint64_t)capacity) bins[dst] = (int32_t)ri;
-            }
+        const Rec &r = frame_recs[ri];
+        fill_one(ri, r.i0, r.i1, r.j0, r.j1, b, ntx, ntiles, tile_offset, tile_cursor, bins, capacity);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // K4: tile raster + resolve
+//
+// Exactness with 32-bit lanes: per (entry, strip) the staging thread evaluates the int64 edge
+// functions at the strip's first pixel, folds in the top-left bias (E + owned > 0  <=>  inside), and
+// classifies each edge over the 16x4 strip: all-outside (entry culled for this strip), all-inside
+// (value pinned to 2^30), or straddling.  For "small" triangles (|A|,|B| < 2^16) a straddling edge
+// satisfies |E| < 2^29 over the strip, so lanes step it with 24-bit multiply-adds exactly; larger
+// triangles fall back to per-lane int64 evaluation.  Results are bit-identical to R3 either way.
+
+constexpr int kStrips = 4;           // waves per tile; a strip is 16 x 4 pixels
+constexpr int kChunk = 256;          // entries staged per round
+constexpr int kSmallEdge = 1 << 16;  // |A|,|B| bound for the 32-bit path
+constexpr uint32_t kStripCulled = 1u, kStripLarge = 2u;
+
+struct alignas(16) StripEdges {
+    int32_t e[3];
+    uint32_t flags;
+};
+struct alignas(16) RasterEntry {  // 128 B of LDS per staged entry
+    StripEdges strip[kStrips];     // 64 B
+    int32_t A[3], B[3];            // 24 B
+    float fx0, fy0, z0, za, zb;    // 20 B
+    int32_t face, ri;              // 8 B
+    int32_t pad[3];
+};
+static_assert(sizeof(RasterEntry) == 128, "RasterEntry must be 128 B");
 
 struct PixelState {
     uint64_t best;
     int32_t best_rec;
 };
 
-__device__ __forceinline__ void raster_one(const RasterPart &R, int32_t ri, int i, int j, PixelState &st)
+__device__ __forceinline__ void depth_update(float za, float zb, float fx0, float fy0, float z0, int32_t face,
+                                             int32_t ri, float fxl, float fyl, PixelState &st)
 {
-    int64_t E[3];
-    edge_values(R, i, j, E);
-    if (!inside(R, E)) return;
-    uint32_t d;
-    if (!sample_depth(R, i, j, d)) return;
-    const uint64_t key = ((uint64_t)d << 32) | (uint32_t)R.face;
+    // R4, same operation order as sample_depth()
+    const float zw = (za * (fxl - fx0) + zb * (fyl - fy0)) + z0;
+    if (!(zw >= 0.0f && zw <= 1.0f)) return;
+    const uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
+    if (q >= kDepthMax) return;
+    const uint64_t key = ((uint64_t)q << 32) | (uint32_t)face;
     if (key < st.best) {
         st.best = key;
         st.best_rec = ri;
     }
 }
 
+__device__ inline void stage_entry(const Rec *__restrict__ frame_recs, int32_t ri, int tx, int ty, RasterEntry &E)
+{
+    const RasterPart R = *reinterpret_cast<const RasterPart *>(&frame_recs[ri]);
+    bool small = true;
+    int64_t owned[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        owned[k] = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
+        small = small && R.A[k] > -kSmallEdge && R.A[k] < kSmallEdge && R.B[k] > -kSmallEdge && R.B[k] < kSmallEdge;
+    }
+#pragma unroll
+    for (int w = 0; w < kStrips; ++w) {
+        const int si0 = tx * kTile, si1 = si0 + kTile - 1, sj0 = ty * kTile + w * 4, sj1 = sj0 + 3;
+        uint32_t flags = 0;
+        int32_t ev[3] = {0, 0, 0};
+        if (R.i1 < si0 || R.i0 > si1 || R.j1 < sj0 || R.j0 > sj1) {
+            flags = kStripCulled;
+        } else if (!small) {
+            flags = kStripLarge;
+        } else {
+            const int64_t px0 = (int64_t)si0 * 256 + 128, py0 = (int64_t)sj0 * 256 + 128;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int64_t e0 = (int64_t)R.A[k] * px0 + (int64_t)R.B[k] * py0 + R.C[k] + owned[k];
+                const int64_t sx = (int64_t)R.A[k] * (15 * 256), sy = (int64_t)R.B[k] * (3 * 256);
+                const int64_t emin = e0 + (sx < 0 ? sx : 0) + (sy < 0 ? sy : 0);
+                const int64_t emax = e0 + (sx > 0 ? sx : 0) + (sy > 0 ? sy : 0);
+                if (emax <= 0) flags = kStripCulled;
+                ev[k] = emin > 0 ? (1 << 30) : (int32_t)e0;
+            }
+        }
+        E.strip[w].e[0] = ev[0]; E.strip[w].e[1] = ev[1]; E.strip[w].e[2] = ev[2];
+        E.strip[w].flags = flags;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { E.A[k] = R.A[k]; E.B[k] = R.B[k]; }
+    E.fx0 = R.fx0; E.fy0 = R.fy0; E.z0 = R.z0; E.za = R.za; E.zb = R.zb;
+    E.face = R.face;
+    E.ri = ri;
+}
+
 template <int CC>
 __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
-                                                     const int32_t *__restrict__ faces, const Rec *__restrict__ recs,
-                                                     const int32_t *__restrict__ nsub,
+                                                     const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ tile_count,
                                                      const uint64_t *__restrict__ tile_offset,
                                                      const int32_t *__restrict__ bins, int64_t capacity,
@@ -379,13 +492,14 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                                                      int64_t nrec, float *__restrict__ pixels, int32_t *__restrict__ gbuffer)
 {
     const int C = CC > 0 ? CC : Cdyn;
-    __shared__ RasterPart lds_rec[256];
-    __shared__ int32_t lds_idx[256];
+    __shared__ RasterEntry lds[kChunk];
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
-    const int t = threadIdx.x, lx = t & 15, ly = t >> 4, wave = t >> 6;
+    const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int i = tx * kTile + lx, j = ty * kTile + ly;
-    const int sx0 = tx * kTile, sx1 = sx0 + kTile - 1, sy0 = ty * kTile + wave * 4, sy1 = sy0 + 3;
+    const int dx = lx * 256, dy = (ly & 3) * 256;
+    const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     PixelState st{~0ull, -1};
 
@@ -393,37 +507,43 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const uint32_t cnt = tile_count[tt];
     const uint64_t off = tile_offset[tt];
     if (off + cnt <= (uint64_t)capacity) {
-        for (uint32_t base = 0; base < cnt; base += 256) {
-            const int n = (int)min(256u, cnt - base);
+        for (uint32_t base = 0; base < cnt; base += kChunk) {
+            const int n = (int)min((uint32_t)kChunk, cnt - base);
             __syncthreads();
-            if (t < n) {
-                const int32_t ri = bins[off + base + t];
-                const uint4 *src = reinterpret_cast<const uint4 *>(frame_recs + ri);
-                uint4 *dst = reinterpret_cast<uint4 *>(&lds_rec[t]);
-#pragma unroll
-                for (int q = 0; q < 5; ++q) dst[q] = src[q];
-                lds_idx[t] = ri;
-            }
+            if (t < n) stage_entry(frame_recs, bins[off + base + t], tx, ty, lds[t]);
             __syncthreads();
             for (int e = 0; e < n; ++e) {
-                const RasterPart &R = lds_rec[e];
-                const int bi0 = __builtin_amdgcn_readfirstlane(R.i0), bi1 = __builtin_amdgcn_readfirstlane(R.i1);
-                const int bj0 = __builtin_amdgcn_readfirstlane(R.j0), bj1 = __builtin_amdgcn_readfirstlane(R.j1);
-                if (bi1 < sx0 || bi0 > sx1 || bj1 < sy0 || bj0 > sy1) continue;
-                raster_one(R, lds_idx[e], i, j, st);
+                const RasterEntry &R = lds[e];
+                const StripEdges se = R.strip[wave];
+                const uint32_t flags = __builtin_amdgcn_readfirstlane(se.flags);
+                if (flags & kStripCulled) continue;
+                bool in;
+                if (!(flags & kStripLarge)) {
+                    const int32_t e0 = se.e[0] + __mul24(R.A[0], dx) + __mul24(R.B[0], dy);
+                    const int32_t e1 = se.e[1] + __mul24(R.A[1], dx) + __mul24(R.B[1], dy);
+                    const int32_t e2 = se.e[2] + __mul24(R.A[2], dx) + __mul24(R.B[2], dy);
+                    in = min(e0, min(e1, e2)) > 0;
+                } else {
+                    const Rec &r = frame_recs[R.ri];
+                    int64_t E[3];
+                    edge_values(r, i, j, E);
+                    in = inside(r, E);
+                }
+                if (in) depth_update(R.za, R.zb, R.fx0, R.fy0, R.z0, R.face, R.ri, fxl, fyl, st);
             }
         }
     } else {
-        // bin overflow (capacity too small for this input): scan every record of the frame
+        // bin overflow (capacity too small for this input): test every record of the frame
         for (int f = 0; f < F; ++f) {
-            const int n = nsub[(int64_t)b * F + f];
-            for (int s = 0; s < n; ++s) {
+            const int ns = fdata[(int64_t)b * F + f].nsub;
+            for (int s = 0; s < ns; ++s) {
                 const int64_t ri = rec_index(F, f, s);
                 const Rec &r = frame_recs[ri];
-                if (r.i0 > r.i1 || r.i1 < sx0 || r.i0 > sx1 || r.j1 < sy0 || r.j0 > sy1) continue;
-                RasterPart R;
-                memcpy(&R, &r, sizeof(RasterPart));
-                raster_one(R, (int32_t)ri, i, j, st);
+                if (r.i0 > r.i1) continue;
+                int64_t E[3];
+                edge_values(r, i, j, E);
+                if (!inside(r, E)) continue;
+                depth_update(r.za, r.zb, r.fx0, r.fy0, r.z0, r.face, (int32_t)ri, fxl, fyl, st);
             }
         }
     }
@@ -438,14 +558,14 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         for (int c = 0; c < C; ++c) out[c] = bg[c];
         return;
     }
-    const Rec r = frame_recs[st.best_rec];
+    const Rec &r = frame_recs[st.best_rec];
+    const FaceData fd = fdata[(int64_t)b * F + face_of_record(st.best_rec, F)];
     int64_t E[3];
     edge_values(r, i, j, E);
     float lam[3] = {0.0f, 0.0f, 0.0f};
     parent_lambda(r, E, lam);
-    const int32_t *f3 = faces + ((int64_t)b * F + r.face) * 3;
     const float *cb = colors + (int64_t)b * V * C;
-    const float *c0 = cb + (int64_t)f3[0] * C, *c1 = cb + (int64_t)f3[1] * C, *c2 = cb + (int64_t)f3[2] * C;
+    const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
     for (int c = 0; c < C; ++c) out[c] = (lam[0] * c0[c] + lam[1] * c1[c]) + lam[2] * c2[c];
 }
 
@@ -458,14 +578,26 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 // on the other side, same-face pairs by the lower lane only).  Reduction without global contention:
 //   1. DPP segmented scan along each 16-pixel row (one DPP row == one pixel row) sums runs of equal
 //      record index into the run's last lane;
-//   2. run tails ds_add into a per-tile LDS hash table keyed by record index;
+//   2. run tails ds_add into a per-tile LDS hash table keyed by record index (vertex ids cached);
 //   3. one wave-instruction of global float atomics per (tile, record): <= 9+3C lanes, ~3 cache lines.
 
-__device__ bool covers_face(const Rec *frame_recs, const int32_t *nsub_frame, int F, int f, int i, int j)
+// Does face f cover pixel (i,j)?  `hint` is a record of f to try first (the one covering a nearby pixel).
+__device__ bool covers_face(const Rec *frame_recs, const FaceData *fdata_frame, int F, int f, int64_t hint, int i, int j)
 {
-    const int n = nsub_frame[f];
+    {
+        const Rec &r = frame_recs[hint];
+        if (!(r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1)) {
+            int64_t E[3];
+            edge_values(r, i, j, E);
+            if (inside(r, E)) return true;
+        }
+    }
+    const int n = fdata_frame[f].nsub;
+    if (n <= 1) return false;
     for (int s = 0; s < n; ++s) {
-        const Rec &r = frame_recs[rec_index(F, f, s)];
+        const int64_t ri = rec_index(F, f, s);
+        if (ri == hint) continue;
+        const Rec &r = frame_recs[ri];
         if (r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1) continue;
         int64_t E[3];
         edge_values(r, i, j, E);
@@ -494,10 +626,9 @@ constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
 constexpr int kHashSlots = 256;    // >= distinct records a 256-pixel tile can hold
 
 template <int CC>
-__global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ verts, const int32_t *__restrict__ faces,
-                                                   const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+__global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
-                                                   const int32_t *__restrict__ nsub, int B, int H, int W, int Cdyn,
+                                                   const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
                                                    int V, int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
                                                    float *__restrict__ grad_colors, float *__restrict__ grad_bg)
 {
@@ -510,6 +641,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
     __shared__ float s_I[kHalo * kHalo * CM];
     __shared__ int32_t s_keys[kHashSlots];
     __shared__ int32_t s_list[kHashSlots];
+    __shared__ int32_t s_vid[kHashSlots * 3];
     __shared__ float s_vals[kHashSlots * NVM];
     __shared__ int32_t s_n;
 
@@ -518,9 +650,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
     const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
     const int i = tx * kTile + lx, j = ty * kTile + ly;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
-    const int32_t *nsub_frame = nsub + (int64_t)b * F;
-    const float *vb = verts + (int64_t)b * V * 4;
-    const int32_t *fb = faces + (int64_t)b * F * 3;
+    const FaceData *fdata_frame = fdata + (int64_t)b * F;
 
     for (int k = t; k < kHashSlots; k += 256) s_keys[k] = -1;
     for (int k = t; k < kHashSlots * NVM; k += 256) s_vals[k] = 0.0f;
@@ -554,12 +684,11 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
 #pragma unroll
     for (int v = 0; v < NVM; ++v) acc[v] = 0.0f;
     int key = -1;
+    FaceData fd;
     if (rp >= 0) {
-        const Rec r = frame_recs[rp];
-        const int f = r.face;
-        const int32_t *f3 = fb + 3 * (int64_t)f;
-        const int v0 = f3[0], v1 = f3[1], v2 = f3[2];
-        const float w0 = vb[(int64_t)v0 * 4 + 3], w1 = vb[(int64_t)v1 * 4 + 3], w2 = vb[(int64_t)v2 * 4 + 3];
+        const Rec &r = frame_recs[rp];
+        const int f = face_of_record(rp, F);
+        fd = fdata_frame[f];
         int64_t Ep[3];
         edge_values(r, i, j, Ep);
         {
@@ -586,15 +715,15 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
             const float s = -0.5f * a;
             if (s == 0.0f) continue;
             const int iq = i + di, jq = j + dj;
-            const int fq = rq >= 0 ? frame_recs[rq].face : -1;
+            const int fq = rq >= 0 ? face_of_record(rq, F) : -1;
             float omega;
             if (fq == f) {
                 omega = me_low ? 1.0f : 0.0f;
             } else if (fq < 0) {
                 omega = 1.0f;
             } else {
-                const bool mine_covers_other = covers_face(frame_recs, nsub_frame, F, f, iq, jq);
-                const bool other_covers_me = covers_face(frame_recs, nsub_frame, F, fq, i, j);
+                const bool mine_covers_other = covers_face(frame_recs, fdata_frame, F, f, rp, iq, jq);
+                const bool other_covers_me = covers_face(frame_recs, fdata_frame, F, fq, rq, i, j);
                 omega = (!mine_covers_other && other_covers_me) ? 1.0f
                         : (mine_covers_other && !other_covers_me) ? 0.0f : 0.5f;
             }
@@ -605,7 +734,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
             for (int k = 0; k < 3; ++k) E[k] = Ep[k] + Eq[k];
             float lam[3];
             if (!parent_lambda(r, E, lam)) continue;
-            const float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
+            const float Wm = (lam[0] * fd.w[0] + lam[1] * fd.w[1]) + lam[2] * fd.w[2];
             if (Wm == 0.0f) continue;
             const int ilo = me_low ? i : iq, jlo = me_low ? j : jq;
             const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
@@ -649,6 +778,9 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
             const int old = atomicCAS(&s_keys[slot], -1, key);
             if (old == -1) {
                 s_list[atomicAdd(&s_n, 1)] = slot;
+                s_vid[slot * 3 + 0] = fd.v[0];
+                s_vid[slot * 3 + 1] = fd.v[1];
+                s_vid[slot * 3 + 2] = fd.v[2];
                 break;
             }
             if (old == key) break;
@@ -663,19 +795,16 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ ver
     const int n = s_n, wave = t >> 6, lane = t & 63;
     float *gvb = grad_verts + (int64_t)b * V * 4;
     float *gcb = grad_colors + (int64_t)b * V * C;
-    for (int e = wave; e < n; e += 4) {
-        const int slot = s_list[e];
-        if (lane >= NV) continue;
-        const float val = s_vals[slot * NVM + lane];
-        if (val == 0.0f) continue;
-        const int f = frame_recs[s_keys[slot]].face;
-        const int32_t *f3 = fb + 3 * (int64_t)f;
-        if (lane < 9) {
-            const int k = lane / 3, comp = lane % 3;
-            atomicAdd(gvb + (int64_t)f3[k] * 4 + (comp == 2 ? 3 : comp), val);
-        } else {
-            const int k = (lane - 9) / C, c = (lane - 9) % C;
-            atomicAdd(gcb + (int64_t)f3[k] * C + c, val);
+    if (lane < NV) {
+        const int k = lane < 9 ? lane / 3 : (lane - 9) / C;
+        const int comp = lane < 9 ? ((lane % 3) == 2 ? 3 : lane % 3) : (lane - 9) % C;
+        for (int e = wave; e < n; e += 4) {
+            const int slot = s_list[e];
+            const float val = s_vals[slot * NVM + lane];
+            if (val == 0.0f) continue;
+            const int vtx = s_vid[slot * 3 + k];
+            if (lane < 9) atomicAdd(gvb + (int64_t)vtx * 4 + comp, val);
+            else atomicAdd(gcb + (int64_t)vtx * C + comp, val);
         }
     }
 }
@@ -693,7 +822,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 1; }
+int dirt_abi_version(void) { return 2; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -731,7 +860,7 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     char *sv = static_cast<char *>(saved), *sc = static_cast<char *>(scratch);
     Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
-    int32_t *nsub = reinterpret_cast<int32_t *>(sv + L.saved_nsub);
+    FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
     uint32_t *tile_count = reinterpret_cast<uint32_t *>(sc + L.off_count);
     uint32_t *tile_cursor = reinterpret_cast<uint32_t *>(sc + L.off_cursor);
     uint64_t *tile_offset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
@@ -739,13 +868,14 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     int32_t *bins = reinterpret_cast<int32_t *>(sc + L.off_bins);
     const int64_t nt = (int64_t)B * L.ntiles;
 
-    // counts and cursors are adjacent: one memset (the flag word is left to dirt_check_faces)
+    // counts and cursors are adjacent: one memset
     HIP_TRY(hipMemsetAsync(tile_count, 0, L.off_offset - L.off_count, stream));
     const int64_t nf = (int64_t)B * F;
+    const unsigned setup_blocks = (unsigned)((nf + kSetupThreads - 1) / kSetupThreads);
     if (nf > 0) {
         ProfScope ps(K_SETUP, stream);
-        setup_kernel<<<dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream>>>(
-            vertices, faces, B, V, F, W, H, L.ntx, L.ntiles, L.nrec, recs, nsub, tile_count, flag);
+        setup_kernel<<<dim3(setup_blocks), dim3(kSetupThreads), 0, stream>>>(
+            vertices, faces, B, V, F, W, H, L.ntx, L.ntiles, L.nrec, recs, fdata, tile_count, flag);
         HIP_TRY(hipGetLastError());
     }
     {
@@ -755,14 +885,14 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     HIP_TRY(hipGetLastError());
     if (nf > 0) {
         ProfScope ps(K_FILL, stream);
-        fill_kernel<<<dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream>>>(
-            recs, nsub, B, F, L.ntx, L.ntiles, L.nrec, tile_offset, tile_cursor, bins, L.bin_capacity);
+        fill_kernel<<<dim3(setup_blocks), dim3(kSetupThreads), 0, stream>>>(
+            recs, fdata, B, F, L.ntx, L.ntiles, L.nrec, tile_offset, tile_cursor, bins, L.bin_capacity);
         HIP_TRY(hipGetLastError());
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
-#define LAUNCH_RASTER(CC)                                                                                       \
-    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, faces, recs, nsub, tile_count,  \
+#define LAUNCH_RASTER(CC)                                                                                        \
+    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, tile_count,         \
                                                       tile_offset, bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, \
                                                       L.ntiles, L.nrec, pixels, gbuffer)
     if (C == 1) LAUNCH_RASTER(1);
@@ -778,12 +908,16 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
                        int V, int F, float *grad_vertices, float *grad_vertex_colors, float *grad_background,
                        void *stream_)
 {
+    // vertices / vertex_colors / faces are part of the contract (rasterise_grad_common.h:19-24); the
+    // forward's FaceData in `saved` already holds what the kernel needs from them.
     (void)vertex_colors;
+    (void)vertices;
+    (void)faces;
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
     if (B == 0) return DIRT_OK;
-    if (!pixels || !grad_pixels || !gbuffer || !saved || !grad_background || (V > 0 && (!grad_vertices || !grad_vertex_colors || !vertices)) ||
-        (F > 0 && !faces))
+    if (!pixels || !grad_pixels || !gbuffer || !saved || !grad_background ||
+        (V > 0 && (!grad_vertices || !grad_vertex_colors)))
         return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
     Layout L;
     rc = make_layout(B, H, W, F, 0, L);
@@ -791,16 +925,16 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     const char *sv = static_cast<const char *>(saved);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
-    const int32_t *nsub = reinterpret_cast<const int32_t *>(sv + L.saved_nsub);
+    const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
     if (V > 0) {
         HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)B * V * 4 * sizeof(float), stream));
         HIP_TRY(hipMemsetAsync(grad_vertex_colors, 0, (size_t)B * V * C * sizeof(float), stream));
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_GRAD, stream);
-#define LAUNCH_GRAD(CC)                                                                                      \
-    grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(vertices, faces, pixels, grad_pixels, gbuffer, recs, nsub, B, H, \
-                                                    W, C, V, F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,   \
+#define LAUNCH_GRAD(CC)                                                                                       \
+    grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, recs, fdata, B, H, W, C, V, F, \
+                                                    L.ntx, L.nrec, grad_vertices, grad_vertex_colors,            \
                                                     grad_background)
     if (C == 1) LAUNCH_GRAD(1);
     else if (C == 3) LAUNCH_GRAD(3);
@@ -842,9 +976,9 @@ int dirt_profile_read(int kernel_id, const char **name, int *launches, double *t
 int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, size_t scratch_bytes, void *stream_)
 {
     if (B < 0 || F < 0 || V < 0) return fail(DIRT_EINVAL, "dirt_check_faces: negative size");
-    if (!scratch || scratch_bytes < 512) return fail(DIRT_EINVAL, "dirt_check_faces: scratch too small");
+    if (!scratch || scratch_bytes < 256) return fail(DIRT_EINVAL, "dirt_check_faces: scratch too small");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
-    uint32_t *flag = reinterpret_cast<uint32_t *>(static_cast<char *>(scratch) + 256 * 0);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(scratch);
     HIP_TRY(hipMemsetAsync(flag, 0, 4, stream));
     const int64_t n = (int64_t)B * F * 3;
     if (n > 0) {

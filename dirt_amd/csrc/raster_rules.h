@@ -41,19 +41,39 @@ struct alignas(16) RasterPart {  // first 80 B of Rec
 };
 static_assert(sizeof(RasterPart) == 80, "RasterPart must be 80 B");
 
+// Per-face data written by setup, read by the resolve and the backward (one 32-B load instead of a
+// faces[] -> vertices[] dependent chain).
+struct alignas(16) FaceData {
+    int32_t v[3];  // vertex indices (frame-local)
+    float w[3];    // clip w of the three parent vertices
+    int32_t nsub;  // number of (sub-)triangle records, 0 = culled
+    int32_t pad;
+};
+static_assert(sizeof(FaceData) == 32, "FaceData must be 32 B");
+
+// Clip-space triangle passed by value (keeps it in registers across the non-inlined clip path).
+struct Tri {
+    float v[3][4];
+};
+
+__host__ __device__ inline int face_of_record(int64_t ri, int F)
+{
+    return ri < F ? (int)ri : (int)((ri - F) / kExtraPerFace);
+}
+
 __host__ __device__ inline int64_t rec_index(int F, int f, int s)
 {
     return s == 0 ? (int64_t)f : (int64_t)F + (int64_t)kExtraPerFace * f + (s - 1);
 }
 
-__device__ inline void set_empty(Rec *r, int face)
+__device__ inline void set_empty(Rec &r, int face)
 {
-    r->i0 = 1; r->i1 = 0; r->j0 = 1; r->j1 = 0;
-    r->face = face;
+    r.i0 = 1; r.i1 = 0; r.j0 = 1; r.j1 = 0;
+    r.face = face;
 }
 
-// R1..R4 for one (sub-)triangle: writes *r, returns true if non-empty.
-__device__ inline bool make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, Rec *r)
+// R1..R4 for one (sub-)triangle: fills `out` (a register-resident local), returns true if non-empty.
+__device__ inline bool make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, Rec &out)
 {
     const float hw = 0.5f * (float)W, hh = 0.5f * (float)H;
     int32_t X[3], Y[3];
@@ -77,7 +97,7 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
         C[k] = -(A[k] * X[a] + B[k] * Y[a]);
     }
     const int64_t D = A[0] * X[0] + B[0] * Y[0] + C[0];
-    if (D == 0) { set_empty(r, face); return false; }
+    if (D == 0) { set_empty(out, face); return false; }
     if (D < 0) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) { A[k] = -A[k]; B[k] = -B[k]; C[k] = -C[k]; }
@@ -90,13 +110,12 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
     j0 = j0 < 0 ? 0 : j0;
     i1 = i1 > W - 1 ? W - 1 : i1;
     j1 = j1 > H - 1 ? H - 1 : j1;
-    if (i0 > i1 || j0 > j1) { set_empty(r, face); return false; }
+    if (i0 > i1 || j0 > j1) { set_empty(out, face); return false; }
     const float fx0 = (float)X[0] * 0.00390625f, fy0 = (float)Y[0] * 0.00390625f;
     const float dx1 = (float)X[1] * 0.00390625f - fx0, dy1 = (float)Y[1] * 0.00390625f - fy0;
     const float dx2 = (float)X[2] * 0.00390625f - fx0, dy2 = (float)Y[2] * 0.00390625f - fy0;
     const float dz1 = zw[1] - zw[0], dz2 = zw[2] - zw[0];
     const float det = (float)D * (1.0f / 65536.0f);
-    Rec out;
 #pragma unroll
     for (int k = 0; k < 3; ++k) { out.A[k] = (int32_t)A[k]; out.B[k] = (int32_t)B[k]; out.C[k] = C[k]; }
     out.i0 = (uint16_t)i0; out.i1 = (uint16_t)i1; out.j0 = (uint16_t)j0; out.j1 = (uint16_t)j1;
@@ -110,7 +129,6 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
 #pragma unroll
         for (int i = 0; i < 3; ++i) out.basis[k * 3 + i] = basis[k][i];
     }
-    *r = out;
     return true;
 }
 
