@@ -84,18 +84,31 @@ inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
 // ------------------------------------------------------------------------------------------------
 // Workspace layout.  saved = records [B][6F] (128 B) + FaceData [B][F] (32 B): what the backward reads.
-// scratch = per-tile counts, cursors, offsets and the bins (forward only).
+// scratch = coarse-tile counts, cursors, offsets and the coarse bins (forward only).
+//
+// Binning is two-level.  Coarse tiles (64x64 px, 128x128 above 4096 px) are binned globally with
+// one device atomic per (workgroup, coarse tile) -- workgroups of 256 faces pre-aggregate in LDS,
+// so the count/fill passes issue ~ncoarse atomics per workgroup instead of one per (face, tile)
+// (scattered device atomics run at ~20 G/s chip-wide on MI355X: 280k of them cost ~14 us).  The
+// fine 16x16-tile / 16x4-strip binning happens inside the raster kernel, per wave, in LDS.
 struct Layout {
-    int ntx, nty, ntiles;
+    int ntx, nty, ntiles;     // fine tiles per frame
+    int cshift, csize;        // coarse tile edge = 1 << cshift pixels
+    int nctx, ncty, ncoarse;  // coarse tiles per frame (<= kMaxCoarse)
     int64_t nrec;
     size_t saved_recs, saved_fdata, saved_total;
     size_t off_count, off_cursor, off_offset, off_flag, off_bins, scratch_total;
     int64_t bin_capacity;
 };
 
-int64_t default_capacity(int B, int F, int ntiles)
+constexpr int kMaxCoarse = 4096;   // LDS histogram size in setup/fill
+constexpr int kFacesPerThread = 1;
+constexpr int kBinThreads = 256;
+constexpr int kFacesPerBlock = kFacesPerThread * kBinThreads;
+
+int64_t default_capacity(int B, int F, int ncoarse)
 {
-    int64_t c = 16 * (int64_t)B * (int64_t)F + 4 * (int64_t)B * ntiles;
+    int64_t c = 8 * (int64_t)B * (int64_t)F + 4 * (int64_t)B * ncoarse;
     if (c < (1 << 20)) c = 1 << 20;
     if (c > 0x7fffffffLL) c = 0x7fffffffLL;
     return c;
@@ -106,19 +119,24 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.ntx = (W + kTile - 1) / kTile;
     L.nty = (H + kTile - 1) / kTile;
     L.ntiles = L.ntx * L.nty;
+    L.cshift = (W <= 4096 && H <= 4096) ? 6 : 7;
+    L.csize = 1 << L.cshift;
+    L.nctx = (W + L.csize - 1) >> L.cshift;
+    L.ncty = (H + L.csize - 1) >> L.cshift;
+    L.ncoarse = L.nctx * L.ncty;
     L.nrec = (int64_t)(1 + kExtraPerFace) * F;
     L.bin_capacity = bin_capacity > 0 ? (bin_capacity > 0x7fffffffLL ? 0x7fffffffLL : bin_capacity)
-                                      : default_capacity(B, F, L.ntiles);
+                                      : default_capacity(B, F, L.ncoarse);
     L.saved_recs = 0;
     L.saved_fdata = (size_t)align_up((int64_t)B * L.nrec * (int64_t)sizeof(Rec), 256);
     L.saved_total = L.saved_fdata + (size_t)align_up((int64_t)B * F * (int64_t)sizeof(FaceData), 256);
-    const int64_t nt = (int64_t)B * L.ntiles;
+    const int64_t nc = (int64_t)B * L.ncoarse;
     size_t o = 0;
-    L.off_count = o;  o += (size_t)align_up(nt * 4, 256);
-    L.off_cursor = o; o += (size_t)align_up(nt * 4, 256);
-    L.off_offset = o; o += (size_t)align_up(nt * 8, 256);
+    L.off_count = o;  o += (size_t)align_up(nc * 4, 256);
+    L.off_cursor = o; o += (size_t)align_up(nc * 4, 256);
+    L.off_offset = o; o += (size_t)align_up(nc * 8, 256);
     L.off_flag = o;   o += 256;
-    L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 4, 256);
+    L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 8, 256);
     L.scratch_total = o;
     return DIRT_OK;
 }
@@ -129,8 +147,8 @@ int validate(int B, int H, int W, int C, int V, int F)
     if (H <= 0 || W <= 0 || H > DIRT_MAX_DIM || W > DIRT_MAX_DIM)
         return fail(DIRT_EINVAL, "Rasterise expects 0 < height, width <= 8192");
     if (C < 1 || C > DIRT_MAX_CHANNELS) return fail(DIRT_EINVAL, "Rasterise expects 1 <= channels <= 8");
-    if ((int64_t)B * F > 0x0fffffffLL || (int64_t)B * V > 0x7fffffffLL)
-        return fail(DIRT_EINVAL, "Rasterise batch too large");
+    if (F > (1 << 26) || (int64_t)B * F > 0x0fffffffLL || (int64_t)B * V > 0x7fffffffLL)
+        return fail(DIRT_EINVAL, "Rasterise batch too large (at most 2^26 faces per frame, 2^28 per batch)");
     return DIRT_OK;
 }
 
@@ -203,56 +221,66 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
     return nsub;
 }
 
-__device__ inline void count_tiles(int i0, int i1, int j0, int j1, int ntx, uint32_t *tile_count_frame)
+// bbox (pixels) packed as i0 | i1<<16 and j0 | j1<<16; empty when i0 > i1
+__device__ __forceinline__ void coarse_range(uint32_t bx, uint32_t by, int cshift, int &cx0, int &cx1, int &cy0, int &cy1)
 {
-    if (i0 > i1) return;
-    const int tx0 = i0 / kTile, tx1 = i1 / kTile, ty0 = j0 / kTile, ty1 = j1 / kTile;
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&tile_count_frame[ty * ntx + tx], 1u);
+    cx0 = (int)(bx & 0xffff) >> cshift;
+    cx1 = (int)(bx >> 16) >> cshift;
+    cy0 = (int)(by & 0xffff) >> cshift;
+    cy1 = (int)(by >> 16) >> cshift;
 }
 
-constexpr int kSetupThreads = 64;  // 50k faces -> 784 workgroups: spread over all 256 CUs
-
-__global__ __launch_bounds__(kSetupThreads) void setup_kernel(const float *__restrict__ verts,
-                                                              const int32_t *__restrict__ faces, int B, int V, int F,
-                                                              int W, int H, int ntx, int ntiles, int64_t nrec,
-                                                              Rec *__restrict__ recs, FaceData *__restrict__ fdata,
-                                                              uint32_t *__restrict__ tile_count, uint32_t *__restrict__ flag)
+__device__ __forceinline__ void load_bbox(const Rec &r, uint32_t &bx, uint32_t &by)
 {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (int64_t)B * F) return;
-    const int b = (int)(gid / F), f = (int)(gid - (int64_t)b * F);
+    const uint2 q = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(&r) + 48);
+    // Rec stores i0, i1, j0, j1 as consecutive uint16
+    bx = q.x;
+    by = q.y;
+}
+
+__global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restrict__ verts,
+                                                            const int32_t *__restrict__ faces, int V, int F, int W,
+                                                            int H, int cshift, int nctx, int ncoarse, int64_t nrec,
+                                                            Rec *__restrict__ recs, FaceData *__restrict__ fdata,
+                                                            uint32_t *__restrict__ ccount, uint32_t *__restrict__ flag)
+{
+    __shared__ uint32_t hist[kMaxCoarse];
+    const int b = blockIdx.y, t = threadIdx.x;
+    for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
+    __syncthreads();
     Rec *frame_recs = recs + (int64_t)b * nrec;
     const float *vb = verts + (int64_t)b * V * 4;
-    const int32_t i0 = faces[gid * 3], i1 = faces[gid * 3 + 1], i2 = faces[gid * 3 + 2];
-    const int32_t vidx[3] = {i0, i1, i2};
-    Tri tri;
-    bool ok = true;
+    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+    for (int q = 0; q < kFacesPerThread; ++q) {
+        const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
+        if (f >= F) break;
+        const int64_t gid = (int64_t)b * F + f;
+        const int32_t i0 = faces[gid * 3], i1 = faces[gid * 3 + 1], i2 = faces[gid * 3 + 2];
+        const int32_t vidx[3] = {i0, i1, i2};
+        Tri tri;
+        bool ok = true;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int32_t vi = vidx[k];
-        if (vi < 0 || vi >= V) {
-            ok = false;
-            tri.v[k][0] = tri.v[k][1] = tri.v[k][2] = 0.0f;
-            tri.v[k][3] = 1.0f;
-        } else {
-            const float4 p = *reinterpret_cast<const float4 *>(vb + (int64_t)vi * 4);
-            tri.v[k][0] = p.x; tri.v[k][1] = p.y; tri.v[k][2] = p.z; tri.v[k][3] = p.w;
-            ok = ok && finite4(tri.v[k]);
+        for (int k = 0; k < 3; ++k) {
+            const int32_t vi = vidx[k];
+            if (vi < 0 || vi >= V) {
+                ok = false;
+                tri.v[k][0] = tri.v[k][1] = tri.v[k][2] = 0.0f;
+                tri.v[k][3] = 1.0f;
+            } else {
+                const float4 p = *reinterpret_cast<const float4 *>(vb + (int64_t)vi * 4);
+                tri.v[k][0] = p.x; tri.v[k][1] = p.y; tri.v[k][2] = p.z; tri.v[k][3] = p.w;
+                ok = ok && finite4(tri.v[k]);
+            }
         }
-    }
-    if (!(i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V)) atomicOr(flag, 1u);
-    uint32_t *tc = tile_count + (int64_t)b * ntiles;
-    FaceData fd;
-    fd.v[0] = i0; fd.v[1] = i1; fd.v[2] = i2;
-    fd.w[0] = tri.v[0][3]; fd.w[1] = tri.v[1][3]; fd.w[2] = tri.v[2][3];
-    fd.pad = 0;
-    Rec r;
-    set_empty(r, f);
-    int nsub = 0;
-    if (ok) {
-        const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
-        bool fast = true;
+        if (!(i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V)) atomicOr(flag, 1u);
+        FaceData fd;
+        fd.v[0] = i0; fd.v[1] = i1; fd.v[2] = i2;
+        fd.w[0] = tri.v[0][3]; fd.w[1] = tri.v[1][3]; fd.w[2] = tri.v[2][3];
+        fd.clipped = 0;
+        Rec r;
+        set_empty(r, f);
+        int nsub = 0;
+        bool fast = ok;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const float w = tri.v[k][3];
@@ -263,24 +291,38 @@ __global__ __launch_bounds__(kSetupThreads) void setup_kernel(const float *__res
             make_record(tri.v, id, W, H, f, r);
             nsub = 1;
             frame_recs[f] = r;
-            count_tiles(r.i0, r.i1, r.j0, r.j1, ntx, tc);
+            if (r.i0 <= r.i1) {
+                const int cx0 = r.i0 >> cshift, cx1 = r.i1 >> cshift, cy0 = r.j0 >> cshift, cy1 = r.j1 >> cshift;
+                for (int cy = cy0; cy <= cy1; ++cy)
+                    for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&hist[cy * nctx + cx], 1u);
+            }
         } else {
             frame_recs[f] = r;  // empty unless clip_face overwrites it
-            nsub = clip_face(tri, W, H, F, f, frame_recs);
+            if (ok) {
+                nsub = clip_face(tri, W, H, F, f, frame_recs);
+                fd.clipped = 1;
+            }
             for (int s = 0; s < nsub; ++s) {
-                const Rec &q = frame_recs[rec_index(F, f, s)];
-                count_tiles(q.i0, q.i1, q.j0, q.j1, ntx, tc);
+                uint32_t bx, by;
+                load_bbox(frame_recs[rec_index(F, f, s)], bx, by);
+                if ((bx & 0xffff) > (bx >> 16)) continue;
+                int cx0, cx1, cy0, cy1;
+                coarse_range(bx, by, cshift, cx0, cx1, cy0, cy1);
+                for (int cy = cy0; cy <= cy1; ++cy)
+                    for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&hist[cy * nctx + cx], 1u);
             }
         }
-    } else {
-        frame_recs[f] = r;
+        fd.nsub = nsub;
+        fdata[gid] = fd;
     }
-    fd.nsub = nsub;
-    fdata[gid] = fd;
+    __syncthreads();
+    uint32_t *cc = ccount + (int64_t)b * ncoarse;
+    for (int c = t; c < ncoarse; c += kBinThreads)
+        if (hist[c]) atomicAdd(&cc[c], hist[c]);
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2: exclusive scan of the per-tile counts (one workgroup; B*ntiles is 4096 per 1024^2 frame)
+// K2: exclusive scan of the per-coarse-tile counts (one workgroup; B*ncoarse is 256 per 1024^2 frame)
 
 constexpr int kScanThreads = 1024;
 constexpr int kScanPerThread = 4;
@@ -336,90 +378,109 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__re
 }
 
 // ------------------------------------------------------------------------------------------------
-// K3: fill bins (order inside a bin is irrelevant: the depth resolve is a commutative min).
-// The common <= 3x3-tile case issues all its returning atomics back to back (one latency, not n).
+// K3: fill the coarse bins.  Entry = {record index, bbox clamped to the coarse tile, 8 bits per side}.
+// Pass 1 counts per coarse tile in LDS, one device atomic per touched coarse tile reserves the
+// workgroup's range, pass 2 hands out positions with LDS atomics.  Order inside a bin is irrelevant
+// (the depth resolve is a commutative min).
 
-__device__ inline void fill_one(int64_t ri, int i0, int i1, int j0, int j1, int b, int ntx, int ntiles,
-                                const uint64_t *__restrict__ tile_offset, uint32_t *__restrict__ tile_cursor,
-                                int32_t *__restrict__ bins, int64_t capacity)
+__device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, int cy, int cshift)
 {
-    if (i0 > i1) return;
-    const int tx0 = i0 / kTile, tx1 = i1 / kTile, ty0 = j0 / kTile, ty1 = j1 / kTile;
-    const int nx = tx1 - tx0 + 1, ny = ty1 - ty0 + 1;
-    const int64_t base = (int64_t)b * ntiles;
-    if (nx <= 3 && ny <= 3) {
-        uint32_t pos[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) {
-            const int qx = q % 3, qy = q / 3;
-            if (qx < nx && qy < ny) pos[q] = atomicAdd(&tile_cursor[base + (ty0 + qy) * ntx + tx0 + qx], 1u);
-        }
-#pragma unroll
-        for (int q = 0; q < 9; ++q) {
-            const int qx = q % 3, qy = q / 3;
-            if (qx < nx && qy < ny) {
-                const int64_t t = base + (ty0 + qy) * ntx + tx0 + qx;
-                const uint64_t dst = tile_offset[t] + pos[q];
-                if (dst < (uint64_t)capacity) bins[dst] = (int32_t)ri;
-            }
-        }
-        return;
-    }
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const int64_t t = base + ty * ntx + tx;
-            const uint32_t pos = atomicAdd(&tile_cursor[t], 1u);
-            const uint64_t dst = tile_offset[t] + pos;
-            if (dst < (uint64_t)capacity) bins[dst] = (int32_t)ri;
-        }
+    const int lim = (1 << cshift) - 1;
+    const int ox = cx << cshift, oy = cy << cshift;
+    const int a0 = max((int)(bx & 0xffff) - ox, 0), a1 = min((int)(bx >> 16) - ox, lim);
+    const int b0 = max((int)(by & 0xffff) - oy, 0), b1 = min((int)(by >> 16) - oy, lim);
+    return (uint32_t)a0 | ((uint32_t)a1 << 8) | ((uint32_t)b0 << 16) | ((uint32_t)b1 << 24);
 }
 
-__global__ __launch_bounds__(kSetupThreads) void fill_kernel(const Rec *__restrict__ recs,
-                                                             const FaceData *__restrict__ fdata, int B, int F, int ntx,
-                                                             int ntiles, int64_t nrec,
-                                                             const uint64_t *__restrict__ tile_offset,
-                                                             uint32_t *__restrict__ tile_cursor,
-                                                             int32_t *__restrict__ bins, int64_t capacity)
+template <bool kPass2>
+__device__ __forceinline__ void bin_face_records(const Rec *__restrict__ frame_recs, int F, int f, int nsub, int cshift,
+                                                 int nctx, uint32_t *hist, const uint64_t *base,
+                                                 uint2 *__restrict__ bins, int64_t capacity)
 {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (int64_t)B * F) return;
-    const int b = (int)(gid / F), f = (int)(gid - (int64_t)b * F);
-    const Rec *frame_recs = recs + (int64_t)b * nrec;
-    const int n = fdata[gid].nsub;
-    for (int s = 0; s < n; ++s) {
+    for (int s = 0; s < nsub; ++s) {
         const int64_t ri = rec_index(F, f, s);
-        const Rec &r = frame_recs[ri];
-        fill_one(ri, r.i0, r.i1, r.j0, r.j1, b, ntx, ntiles, tile_offset, tile_cursor, bins, capacity);
+        uint32_t bx, by;
+        load_bbox(frame_recs[ri], bx, by);
+        if ((bx & 0xffff) > (bx >> 16)) continue;
+        int cx0, cx1, cy0, cy1;
+        coarse_range(bx, by, cshift, cx0, cx1, cy0, cy1);
+        for (int cy = cy0; cy <= cy1; ++cy)
+            for (int cx = cx0; cx <= cx1; ++cx) {
+                const int c = cy * nctx + cx;
+                if (!kPass2) {
+                    atomicAdd(&hist[c], 1u);
+                } else {
+                    const uint64_t dst = base[c] + atomicAdd(&hist[c], 1u);
+                    if (dst < (uint64_t)capacity) bins[dst] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
+                }
+            }
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict__ recs,
+                                                           const FaceData *__restrict__ fdata, int F, int cshift,
+                                                           int nctx, int ncoarse, int64_t nrec,
+                                                           const uint64_t *__restrict__ coffset,
+                                                           uint32_t *__restrict__ ccursor, uint2 *__restrict__ bins,
+                                                           int64_t capacity)
+{
+    __shared__ uint32_t hist[kMaxCoarse];
+    __shared__ uint64_t base[kMaxCoarse];
+    const int b = blockIdx.y, t = threadIdx.x;
+    for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
+    __syncthreads();
+    const Rec *frame_recs = recs + (int64_t)b * nrec;
+    int nsub[kFacesPerThread];
+#pragma unroll
+    for (int q = 0; q < kFacesPerThread; ++q) {
+        const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
+        nsub[q] = f < F ? fdata[(int64_t)b * F + f].nsub : 0;
+        bin_face_records<false>(frame_recs, F, f, nsub[q], cshift, nctx, hist, nullptr, bins, capacity);
+    }
+    __syncthreads();
+    const int64_t cb = (int64_t)b * ncoarse;
+    for (int c = t; c < ncoarse; c += kBinThreads) {
+        const uint32_t n = hist[c];
+        if (n) base[c] = coffset[cb + c] + atomicAdd(&ccursor[cb + c], n);
+        hist[c] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kFacesPerThread; ++q) {
+        const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
+        bin_face_records<true>(frame_recs, F, f, nsub[q], cshift, nctx, hist, base, bins, capacity);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // K4: tile raster + resolve
 //
-// Exactness with 32-bit lanes: per (entry, strip) the staging thread evaluates the int64 edge
-// functions at the strip's first pixel, folds in the top-left bias (E + owned > 0  <=>  inside), and
-// classifies each edge over the 16x4 strip: all-outside (entry culled for this strip), all-inside
-// (value pinned to 2^30), or straddling.  For "small" triangles (|A|,|B| < 2^16) a straddling edge
-// satisfies |E| < 2^29 over the strip, so lanes step it with 24-bit multiply-adds exactly; larger
-// triangles fall back to per-lane int64 evaluation.  Results are bit-identical to R3 either way.
+// One workgroup per 16x16 tile; each of its 4 waves owns a 16x4 strip and works independently of
+// the others (wave-private LDS, no workgroup barriers):
+//   a. filter the coarse bin by the packed bbox against the strip, compacting survivors (ballot);
+//   b. per survivor (one lane each) evaluate the int64 edge functions at the strip origin, fold in
+//      the top-left bias (E + owned > 0 <=> inside) and classify each edge over the strip:
+//      all-outside -> dropped, all-inside -> pinned to 2^30, straddling -> exact int32 value;
+//      survivors are compacted again into a 64-B LDS entry;
+//   c. every lane (pixel) steps the three edges with 24-bit multiply-adds -- exact for triangles
+//      with |A|,|B| < 2^16 (|E| < 2^29 over a strip); larger ones use per-lane int64 (flagged) --
+//      and keeps the min (depth24<<32 | face) key.
+// Results are bit-identical to R3/R4 (oracle) by construction.
 
-constexpr int kStrips = 4;           // waves per tile; a strip is 16 x 4 pixels
-constexpr int kChunk = 256;          // entries staged per round
-constexpr int kSmallEdge = 1 << 16;  // |A|,|B| bound for the 32-bit path
-constexpr uint32_t kStripCulled = 1u, kStripLarge = 2u;
+constexpr int kStrips = 4;
+constexpr int kSmallEdge = 1 << 16;
+constexpr int kListCap = 512;      // per-wave survivor list (filtered record indices)
+constexpr int32_t kLargeFlag = (int32_t)0x80000000;
 
-struct alignas(16) StripEdges {
+struct alignas(16) StripEntry {  // 64 B of wave-private LDS per staged triangle
     int32_t e[3];
-    uint32_t flags;
+    int32_t A[3];
+    int32_t B[3];
+    float za, zb, fx0, fy0, z0;
+    int32_t face;
+    int32_t ri;  // record index; kLargeFlag set -> per-lane int64 path
 };
-struct alignas(16) RasterEntry {  // 128 B of LDS per staged entry
-    StripEdges strip[kStrips];     // 64 B
-    int32_t A[3], B[3];            // 24 B
-    float fx0, fy0, z0, za, zb;    // 20 B
-    int32_t face, ri;              // 8 B
-    int32_t pad[3];
-};
-static_assert(sizeof(RasterEntry) == 128, "RasterEntry must be 128 B");
+static_assert(sizeof(StripEntry) == 64, "StripEntry must be 64 B");
 
 struct PixelState {
     uint64_t best;
@@ -441,96 +502,156 @@ __device__ __forceinline__ void depth_update(float za, float zb, float fx0, floa
     }
 }
 
-__device__ inline void stage_entry(const Rec *__restrict__ frame_recs, int32_t ri, int tx, int ty, RasterEntry &E)
+__device__ __forceinline__ void wave_lds_sync()
 {
-    const RasterPart R = *reinterpret_cast<const RasterPart *>(&frame_recs[ri]);
-    bool small = true;
-    int64_t owned[3];
+    // LDS ops of one wave execute in order; this only stops the compiler from reordering across it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Stage up to 64 survivors (s_list[from .. from+m)) into entries; returns number staged.
+__device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_list, int from, int m, int si0, int sj0,
+                           StripEntry *ent, int lane)
+{
+    bool keep = false;
+    StripEntry E;
+    if (lane < m) {
+        const int32_t ri = s_list[from + lane];
+        const RasterPart R = *reinterpret_cast<const RasterPart *>(&frame_recs[ri]);
+        bool small = true;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        owned[k] = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
-        small = small && R.A[k] > -kSmallEdge && R.A[k] < kSmallEdge && R.B[k] > -kSmallEdge && R.B[k] < kSmallEdge;
-    }
+        for (int k = 0; k < 3; ++k)
+            small = small && R.A[k] > -kSmallEdge && R.A[k] < kSmallEdge && R.B[k] > -kSmallEdge && R.B[k] < kSmallEdge;
+        keep = true;
+        const int64_t px0 = (int64_t)si0 * 256 + 128, py0 = (int64_t)sj0 * 256 + 128;
 #pragma unroll
-    for (int w = 0; w < kStrips; ++w) {
-        const int si0 = tx * kTile, si1 = si0 + kTile - 1, sj0 = ty * kTile + w * 4, sj1 = sj0 + 3;
-        uint32_t flags = 0;
-        int32_t ev[3] = {0, 0, 0};
-        if (R.i1 < si0 || R.i0 > si1 || R.j1 < sj0 || R.j0 > sj1) {
-            flags = kStripCulled;
-        } else if (!small) {
-            flags = kStripLarge;
-        } else {
-            const int64_t px0 = (int64_t)si0 * 256 + 128, py0 = (int64_t)sj0 * 256 + 128;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int64_t e0 = (int64_t)R.A[k] * px0 + (int64_t)R.B[k] * py0 + R.C[k] + owned[k];
-                const int64_t sx = (int64_t)R.A[k] * (15 * 256), sy = (int64_t)R.B[k] * (3 * 256);
-                const int64_t emin = e0 + (sx < 0 ? sx : 0) + (sy < 0 ? sy : 0);
-                const int64_t emax = e0 + (sx > 0 ? sx : 0) + (sy > 0 ? sy : 0);
-                if (emax <= 0) flags = kStripCulled;
-                ev[k] = emin > 0 ? (1 << 30) : (int32_t)e0;
-            }
+        for (int k = 0; k < 3; ++k) {
+            const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
+            const int64_t e0 = (int64_t)R.A[k] * px0 + (int64_t)R.B[k] * py0 + R.C[k] + owned;
+            const int64_t sx = (int64_t)R.A[k] * (15 * 256), sy = (int64_t)R.B[k] * (3 * 256);
+            const int64_t emin = e0 + (sx < 0 ? sx : 0) + (sy < 0 ? sy : 0);
+            const int64_t emax = e0 + (sx > 0 ? sx : 0) + (sy > 0 ? sy : 0);
+            if (emax <= 0) keep = false;
+            E.e[k] = emin > 0 ? (1 << 30) : (int32_t)e0;
+            E.A[k] = R.A[k];
+            E.B[k] = R.B[k];
         }
-        E.strip[w].e[0] = ev[0]; E.strip[w].e[1] = ev[1]; E.strip[w].e[2] = ev[2];
-        E.strip[w].flags = flags;
+        E.za = R.za; E.zb = R.zb; E.fx0 = R.fx0; E.fy0 = R.fy0; E.z0 = R.z0;
+        E.face = R.face;
+        E.ri = small ? ri : (ri | kLargeFlag);
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { E.A[k] = R.A[k]; E.B[k] = R.B[k]; }
-    E.fx0 = R.fx0; E.fy0 = R.fy0; E.z0 = R.z0; E.za = R.za; E.zb = R.zb;
-    E.face = R.face;
-    E.ri = ri;
+    const uint64_t mask = __ballot(keep);
+    if (keep) {
+        const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        ent[pos] = E;
+    }
+    return __popcll(mask);
 }
 
 template <int CC>
 __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
-                                                     const uint32_t *__restrict__ tile_count,
-                                                     const uint64_t *__restrict__ tile_offset,
-                                                     const int32_t *__restrict__ bins, int64_t capacity,
-                                                     int B, int H, int W, int Cdyn, int V, int F, int ntx, int ntiles,
-                                                     int64_t nrec, float *__restrict__ pixels, int32_t *__restrict__ gbuffer)
+                                                     const uint32_t *__restrict__ ccount,
+                                                     const uint64_t *__restrict__ coffset,
+                                                     const uint2 *__restrict__ bins, int64_t capacity,
+                                                     int B, int H, int W, int Cdyn, int V, int F, int ntx, int cshift,
+                                                     int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
+                                                     int32_t *__restrict__ gbuffer)
 {
+    constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     const int C = CC > 0 ? CC : Cdyn;
-    __shared__ RasterEntry lds[kChunk];
+    __shared__ int32_t s_list_all[kStrips][kListCap];
+    __shared__ StripEntry s_ent_all[kStrips][64];
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
-    const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
+    const int t = threadIdx.x, lx = t & 15, ly = t >> 4, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    int32_t *s_list = s_list_all[wave];
+    StripEntry *s_ent = s_ent_all[wave];
     const int i = tx * kTile + lx, j = ty * kTile + ly;
     const int dx = lx * 256, dy = (ly & 3) * 256;
     const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
-    PixelState st{~0ull, -1};
+    const bool in_frame = i < W && j < H;
+    const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
 
-    const int64_t tt = (int64_t)b * ntiles + tile;
-    const uint32_t cnt = tile_count[tt];
-    const uint64_t off = tile_offset[tt];
+    // prefetch the background of this pixel (used if nothing covers it)
+    float bgv[CM];
+    if (in_frame) {
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < C) bgv[c] = background[o * C + c];
+    }
+
+    PixelState st{~0ull, -1};
+    const int si0 = tx * kTile, sj0 = ty * kTile + wave * 4;
+    const int cx = si0 >> cshift, cy = sj0 >> cshift;
+    const int c = cy * nctx + cx;
+    const int64_t cc = (int64_t)b * ncoarse + c;
+    const uint32_t cnt = ccount[cc];
+    const uint64_t off = coffset[cc];
+    // strip rectangle relative to the coarse tile
+    const uint32_t rx0 = (uint32_t)(si0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
+    const uint32_t ry0 = (uint32_t)(sj0 - (cy << cshift)), ry1 = ry0 + 3;
+
     if (off + cnt <= (uint64_t)capacity) {
-        for (uint32_t base = 0; base < cnt; base += kChunk) {
-            const int n = (int)min((uint32_t)kChunk, cnt - base);
-            __syncthreads();
-            if (t < n) stage_entry(frame_recs, bins[off + base + t], tx, ty, lds[t]);
-            __syncthreads();
-            for (int e = 0; e < n; ++e) {
-                const RasterEntry &R = lds[e];
-                const StripEdges se = R.strip[wave];
-                const uint32_t flags = __builtin_amdgcn_readfirstlane(se.flags);
-                if (flags & kStripCulled) continue;
-                bool in;
-                if (!(flags & kStripLarge)) {
-                    const int32_t e0 = se.e[0] + __mul24(R.A[0], dx) + __mul24(R.B[0], dy);
-                    const int32_t e1 = se.e[1] + __mul24(R.A[1], dx) + __mul24(R.B[1], dy);
-                    const int32_t e2 = se.e[2] + __mul24(R.A[2], dx) + __mul24(R.B[2], dy);
-                    in = min(e0, min(e1, e2)) > 0;
-                } else {
-                    const Rec &r = frame_recs[R.ri];
-                    int64_t E[3];
-                    edge_values(r, i, j, E);
-                    in = inside(r, E);
+        int n_s = 0;
+        for (uint32_t blk = 0;; blk += 256) {
+            const bool more = blk < cnt;
+            if (more) {
+                // a. filter the coarse bin (4 independent loads per lane in flight)
+                uint2 ev[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t idx = blk + u * 64 + lane;
+                    ok[u] = idx < cnt;
+                    ev[u] = ok[u] ? bins[off + idx] : make_uint2(0u, 0u);
                 }
-                if (in) depth_update(R.za, R.zb, R.fx0, R.fy0, R.z0, R.face, R.ri, fxl, fyl, st);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t bb = ev[u].y;
+                    const bool keep = ok[u] && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 &&
+                                      ((bb >> 16) & 0xff) <= ry1 && (bb >> 24) >= ry0;
+                    const uint64_t mask = __ballot(keep);
+                    if (keep) {
+                        const int pos = n_s + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                        s_list[pos] = (int32_t)ev[u].x;
+                    }
+                    n_s += __popcll(mask);
+                }
             }
+            if (n_s == 0 && !more) break;
+            if (n_s < kListCap - 256 && more) continue;
+            wave_lds_sync();
+            // b + c: stage and rasterise the collected survivors, 64 at a time
+            for (int from = 0; from < n_s; from += 64) {
+                const int m = min(64, n_s - from);
+                const int ne = stage_strip(frame_recs, s_list, from, m, si0, sj0, s_ent, lane);
+                wave_lds_sync();
+                for (int e = 0; e < ne; ++e) {
+                    const StripEntry &R = s_ent[e];
+                    const int32_t rif = __builtin_amdgcn_readfirstlane(R.ri);
+                    bool in;
+                    if (rif >= 0) {
+                        const int32_t e0 = R.e[0] + __mul24(R.A[0], dx) + __mul24(R.B[0], dy);
+                        const int32_t e1 = R.e[1] + __mul24(R.A[1], dx) + __mul24(R.B[1], dy);
+                        const int32_t e2 = R.e[2] + __mul24(R.A[2], dx) + __mul24(R.B[2], dy);
+                        in = min(e0, min(e1, e2)) > 0;
+                    } else {
+                        const Rec &r = frame_recs[rif & 0x7fffffff];
+                        int64_t E[3];
+                        edge_values(r, i, j, E);
+                        in = inside(r, E);
+                    }
+                    if (in) depth_update(R.za, R.zb, R.fx0, R.fy0, R.z0, R.face, rif & 0x7fffffff, fxl, fyl, st);
+                }
+                wave_lds_sync();
+            }
+            n_s = 0;
+            if (!more) break;
         }
     } else {
         // bin overflow (capacity too small for this input): test every record of the frame
@@ -548,25 +669,25 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         }
     }
 
-    if (i >= W || j >= H) return;
-    const int row = H - 1 - j;
-    const int64_t o = ((int64_t)b * H + row) * W + i;
-    gbuffer[o] = st.best_rec;
+    if (!in_frame) return;
     float *out = pixels + o * C;
     if (st.best_rec < 0) {
-        const float *bg = background + o * C;
-        for (int c = 0; c < C; ++c) out[c] = bg[c];
+        gbuffer[o] = -1;
+#pragma unroll
+        for (int c2 = 0; c2 < CM; ++c2)
+            if (c2 < C) out[c2] = bgv[c2];
         return;
     }
     const Rec &r = frame_recs[st.best_rec];
     const FaceData fd = fdata[(int64_t)b * F + face_of_record(st.best_rec, F)];
+    gbuffer[o] = st.best_rec | (fd.clipped ? kGbufMulti : 0);
     int64_t E[3];
     edge_values(r, i, j, E);
     float lam[3] = {0.0f, 0.0f, 0.0f};
     parent_lambda(r, E, lam);
     const float *cb = colors + (int64_t)b * V * C;
     const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
-    for (int c = 0; c < C; ++c) out[c] = (lam[0] * c0[c] + lam[1] * c1[c]) + lam[2] * c2[c];
+    for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -581,27 +702,26 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 //   2. run tails ds_add into a per-tile LDS hash table keyed by record index (vertex ids cached);
 //   3. one wave-instruction of global float atomics per (tile, record): <= 9+3C lanes, ~3 cache lines.
 
-// Does face f cover pixel (i,j)?  `hint` is a record of f to try first (the one covering a nearby pixel).
-__device__ bool covers_face(const Rec *frame_recs, const FaceData *fdata_frame, int F, int f, int64_t hint, int i, int j)
+// Does face f cover pixel (i,j)?  `hint` is the record of f covering a neighbouring pixel; the other
+// sub-records of f are only consulted when f was clipped into several (`multi`).
+__device__ __forceinline__ bool edge_covers(const EdgePart &r, int i, int j)
 {
-    {
-        const Rec &r = frame_recs[hint];
-        if (!(r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1)) {
-            int64_t E[3];
-            edge_values(r, i, j, E);
-            if (inside(r, E)) return true;
-        }
-    }
+    if (r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1) return false;
+    int64_t E[3];
+    edge_values(r, i, j, E);
+    return inside(r, E);
+}
+
+__device__ bool covers_face(const EdgePart &hint, int64_t hint_ri, bool multi, const Rec *frame_recs,
+                            const FaceData *fdata_frame, int F, int f, int i, int j)
+{
+    if (edge_covers(hint, i, j)) return true;
+    if (!multi) return false;
     const int n = fdata_frame[f].nsub;
-    if (n <= 1) return false;
     for (int s = 0; s < n; ++s) {
         const int64_t ri = rec_index(F, f, s);
-        if (ri == hint) continue;
-        const Rec &r = frame_recs[ri];
-        if (r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1) continue;
-        int64_t E[3];
-        edge_values(r, i, j, E);
-        if (inside(r, E)) return true;
+        if (ri == hint_ri) continue;
+        if (edge_covers(*reinterpret_cast<const EdgePart *>(&frame_recs[ri]), i, j)) return true;
     }
     return false;
 }
@@ -620,6 +740,30 @@ template <int D>
 __device__ __forceinline__ int dpp_shl_i(int v, int fill)  // lane l <- lane l+D of the same row
 {
     return __builtin_amdgcn_update_dpp(fill, v, 0x100 + D, 0xF, 0xF, false);
+}
+
+// int64 -> f32 with two conversions (may double-round: backward-only, tolerance-level)
+__device__ __forceinline__ float fast_i64_to_f32(int64_t v)
+{
+    const int32_t hi = (int32_t)(v >> 32);
+    const uint32_t lo = (uint32_t)v;
+    return fmaf((float)hi, 4294967296.0f, (float)lo);
+}
+
+// perspective-correct barycentrics from a_k = E_k / w_k (R6) with one fast reciprocal
+__device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, float a1, float a2, float lam[3])
+{
+    const float s = (a0 + a1) + a2;
+    if (s == 0.0f) return false;
+    const float rs = __builtin_amdgcn_rcpf(s);
+    const float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
+    if (!multi) {
+        lam[0] = m0; lam[1] = m1; lam[2] = m2;
+        return true;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
+    return true;
 }
 
 constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
@@ -651,6 +795,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     const int i = tx * kTile + lx, j = ty * kTile + ly;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
+    const float inv_hw = 2.0f / (float)W, inv_hh = 2.0f / (float)H;
 
     for (int k = t; k < kHashSlots; k += 256) s_keys[k] = -1;
     for (int k = t; k < kHashSlots * NVM; k += 256) s_vals[k] = 0.0f;
@@ -674,7 +819,8 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
 
     const bool in_frame = i < W && j < H;
     const int kme = (ly + 1) * kHalo + (lx + 1);
-    const int32_t rp = in_frame ? s_rec[kme] : -2;
+    const int32_t gp = in_frame ? s_rec[kme] : -2;
+    const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
     if (in_frame) {
         const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
         for (int c = 0; c < C; ++c) grad_bg[o * C + c] = rp < 0 ? s_G[kme * CM + c] : 0.0f;
@@ -686,18 +832,38 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     int key = -1;
     FaceData fd;
     if (rp >= 0) {
-        const Rec &r = frame_recs[rp];
+        // Every global load this lane needs is issued up front: the own record's edges, 1/w and (only
+        // for clipped faces) basis, the face data, and the edge part of each neighbour's record where
+        // the neighbour shows a different face.  Ownership decisions (covers tests) are exact int64;
+        // the interpolation weights use fast reciprocals (contributions agree with the oracle to
+        // ~1e-6 relative, far inside the 1e-4 tolerance the atomic summation order already needs).
         const int f = face_of_record(rp, F);
+        const bool multi = (gp & kGbufMulti) != 0;
+        const Rec &rr = frame_recs[rp];
+        const EdgePart mine = *reinterpret_cast<const EdgePart *>(&rr);
+        const float iw0 = rr.iw[0], iw1 = rr.iw[1], iw2 = rr.iw[2];
         fd = fdata_frame[f];
-        int64_t Ep[3];
-        edge_values(r, i, j, Ep);
-        {
-            float lam[3];
-            if (parent_lambda(r, Ep, lam)) {
+        int32_t gq[4], fqv[4];
+        EdgePart nb[4];
 #pragma unroll
-                for (int k = 0; k < 3; ++k)
-                    for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * s_G[kme * CM + c];
-            }
+        for (int dir = 0; dir < 4; ++dir) {
+            const int axis = dir >> 1, sgn = (dir & 1) ? -1 : 1;
+            const int kq = kme + (axis == 1 ? sgn * kHalo : 0) + (axis == 0 ? sgn : 0);
+            gq[dir] = s_rec[kq];
+            fqv[dir] = gq[dir] >= 0 ? face_of_record(gq[dir] & kGbufIndexMask, F) : -1;
+            if (fqv[dir] >= 0 && fqv[dir] != f)
+                nb[dir] = *reinterpret_cast<const EdgePart *>(&frame_recs[gq[dir] & kGbufIndexMask]);
+        }
+        int64_t Ep[3];
+        edge_values(mine, i, j, Ep);
+        float fEp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fEp[k] = fast_i64_to_f32(Ep[k]);
+        float lam[3];
+        if (fast_lambda(rr, multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * s_G[kme * CM + c];
         }
         // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window)
 #pragma unroll
@@ -706,8 +872,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             const bool me_low = (dir & 1) == 0;
             const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
             const int kq = kme + dj * kHalo + di;
-            const int32_t rq = s_rec[kq];
-            if (rq == -2) continue;
+            if (gq[dir] == -2) continue;
             const int klo = me_low ? kme : kq, kup = me_low ? kq : kme;
             float a = 0.0f;
             for (int c = 0; c < C; ++c)
@@ -715,37 +880,47 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             const float s = -0.5f * a;
             if (s == 0.0f) continue;
             const int iq = i + di, jq = j + dj;
-            const int fq = rq >= 0 ? face_of_record(rq, F) : -1;
+            const int fq = fqv[dir];
+            // exact edge values of this face at the neighbour: one step of 256 sub-pixels
+            int64_t step[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) step[k] = (int64_t)(axis == 0 ? mine.A[k] : mine.B[k]) * (me_low ? 256 : -256);
             float omega;
             if (fq == f) {
                 omega = me_low ? 1.0f : 0.0f;
             } else if (fq < 0) {
                 omega = 1.0f;
             } else {
-                const bool mine_covers_other = covers_face(frame_recs, fdata_frame, F, f, rp, iq, jq);
-                const bool other_covers_me = covers_face(frame_recs, fdata_frame, F, fq, rq, i, j);
+                int64_t Eq[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) Eq[k] = Ep[k] + step[k];
+                bool mine_covers_other = inside(mine, Eq);
+                if (!mine_covers_other && multi)
+                    mine_covers_other = covers_face(mine, rp, true, frame_recs, fdata_frame, F, f, iq, jq);
+                const bool other_covers_me = covers_face(nb[dir], gq[dir] & kGbufIndexMask, (gq[dir] & kGbufMulti) != 0,
+                                                         frame_recs, fdata_frame, F, fq, i, j);
                 omega = (!mine_covers_other && other_covers_me) ? 1.0f
                         : (mine_covers_other && !other_covers_me) ? 0.0f : 0.5f;
             }
             if (omega == 0.0f) continue;
-            int64_t Eq[3], E[3];
-            edge_values(r, iq, jq, Eq);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) E[k] = Ep[k] + Eq[k];
-            float lam[3];
-            if (!parent_lambda(r, E, lam)) continue;
-            const float Wm = (lam[0] * fd.w[0] + lam[1] * fd.w[1]) + lam[2] * fd.w[2];
+            // midpoint: E(p) + E(q) = 2 E(p) + step
+            const float m0 = (2.0f * fEp[0] + (float)step[0]) * iw0;
+            const float m1 = (2.0f * fEp[1] + (float)step[1]) * iw1;
+            const float m2 = (2.0f * fEp[2] + (float)step[2]) * iw2;
+            float lm[3];
+            if (!fast_lambda(rr, multi, m0, m1, m2, lm)) continue;
+            const float Wm = (lm[0] * fd.w[0] + lm[1] * fd.w[1]) + lm[2] * fd.w[2];
             if (Wm == 0.0f) continue;
             const int ilo = me_low ? i : iq, jlo = me_low ? j : jq;
             const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
             const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
-            const float ndc = mid / half - 1.0f;
-            const float tt = ((omega * s) * half) / Wm;
+            const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
+            const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                const float g = tt * lam[k];
+                const float g = tt * lm[k];
                 acc[k * 3 + axis] += g;
-                acc[k * 3 + 2] += -(g * ndc);
+                acc[k * 3 + 2] -= g * ndc;
             }
         }
         key = rp;
@@ -861,40 +1036,39 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     char *sv = static_cast<char *>(saved), *sc = static_cast<char *>(scratch);
     Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
     FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
-    uint32_t *tile_count = reinterpret_cast<uint32_t *>(sc + L.off_count);
-    uint32_t *tile_cursor = reinterpret_cast<uint32_t *>(sc + L.off_cursor);
-    uint64_t *tile_offset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
+    uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
+    uint32_t *ccursor = reinterpret_cast<uint32_t *>(sc + L.off_cursor);
+    uint64_t *coffset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
     uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
-    int32_t *bins = reinterpret_cast<int32_t *>(sc + L.off_bins);
-    const int64_t nt = (int64_t)B * L.ntiles;
+    uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
+    const int64_t nc = (int64_t)B * L.ncoarse;
 
     // counts and cursors are adjacent: one memset
-    HIP_TRY(hipMemsetAsync(tile_count, 0, L.off_offset - L.off_count, stream));
-    const int64_t nf = (int64_t)B * F;
-    const unsigned setup_blocks = (unsigned)((nf + kSetupThreads - 1) / kSetupThreads);
-    if (nf > 0) {
+    HIP_TRY(hipMemsetAsync(ccount, 0, L.off_offset - L.off_count, stream));
+    const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
+    if (F > 0) {
         ProfScope ps(K_SETUP, stream);
-        setup_kernel<<<dim3(setup_blocks), dim3(kSetupThreads), 0, stream>>>(
-            vertices, faces, B, V, F, W, H, L.ntx, L.ntiles, L.nrec, recs, fdata, tile_count, flag);
+        setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag);
         HIP_TRY(hipGetLastError());
     }
     {
         ProfScope ps(K_SCAN, stream);
-        scan_kernel<<<dim3(1), dim3(kScanThreads), 0, stream>>>(tile_count, tile_offset, nt);
+        scan_kernel<<<dim3(1), dim3(kScanThreads), 0, stream>>>(ccount, coffset, nc);
     }
     HIP_TRY(hipGetLastError());
-    if (nf > 0) {
+    if (F > 0) {
         ProfScope ps(K_FILL, stream);
-        fill_kernel<<<dim3(setup_blocks), dim3(kSetupThreads), 0, stream>>>(
-            recs, fdata, B, F, L.ntx, L.ntiles, L.nrec, tile_offset, tile_cursor, bins, L.bin_capacity);
+        fill_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(recs, fdata, F, L.cshift, L.nctx, L.ncoarse, L.nrec,
+                                                                coffset, ccursor, bins, L.bin_capacity);
         HIP_TRY(hipGetLastError());
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
 #define LAUNCH_RASTER(CC)                                                                                        \
-    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, tile_count,         \
-                                                      tile_offset, bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, \
-                                                      L.ntiles, L.nrec, pixels, gbuffer)
+    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, coffset,    \
+                                                      bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift,    \
+                                                      L.nctx, L.ncoarse, L.nrec, pixels, gbuffer)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else LAUNCH_RASTER(0);

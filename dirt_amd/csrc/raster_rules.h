@@ -17,6 +17,10 @@ constexpr int kTile = 16;          // raster tile edge (pixels); one 256-thread 
 constexpr int kMaxSub = 6;         // fan triangles of a triangle clipped by 5 planes
 constexpr int kExtraPerFace = 5;   // record slots F + 5f + (s-1) for sub-triangles s>0
 constexpr uint32_t kDepthMax = 16777215u;  // 2^24-1 == cleared depth 1.0 (rasterise_egl.cpp:449)
+// g-buffer word: visible record index (< 2^29 since F <= 2^26), bit 30 set when the face went through
+// the R5 clipping path (non-identity basis, possibly several records), -1 for background
+constexpr int32_t kGbufMulti = 1 << 30;
+constexpr int32_t kGbufIndexMask = kGbufMulti - 1;
 
 // Per (sub-)triangle setup record, 128 B.  The first 80 B are what the tile raster stages in LDS.
 struct alignas(16) Rec {
@@ -30,6 +34,14 @@ struct alignas(16) Rec {
     float basis[9];              // row k = parent barycentric of sub-vertex k (identity on the fast path)
 };
 static_assert(sizeof(Rec) == 128, "Rec must be 128 B");
+
+struct alignas(8) EdgePart {  // first 56 B of Rec: what a coverage test needs
+    int32_t A[3];
+    int32_t B[3];
+    int64_t C[3];
+    uint16_t i0, i1, j0, j1;
+};
+static_assert(sizeof(EdgePart) == 56, "EdgePart must be 56 B");
 
 struct alignas(16) RasterPart {  // first 80 B of Rec
     int32_t A[3];
@@ -46,8 +58,8 @@ static_assert(sizeof(RasterPart) == 80, "RasterPart must be 80 B");
 struct alignas(16) FaceData {
     int32_t v[3];  // vertex indices (frame-local)
     float w[3];    // clip w of the three parent vertices
-    int32_t nsub;  // number of (sub-)triangle records, 0 = culled
-    int32_t pad;
+    int32_t nsub;     // number of (sub-)triangle records, 0 = culled
+    int32_t clipped;  // 1 if set up by the R5 clipping path
 };
 static_assert(sizeof(FaceData) == 32, "FaceData must be 32 B");
 

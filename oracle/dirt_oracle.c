@@ -55,6 +55,9 @@
 #define MAX_SUB 6 /* a triangle clipped by 5 planes has <= 8 vertices -> <= 6 fan triangles */
 #define MAX_POLY 9
 #define DEPTH_MAX 16777215u
+/* g-buffer word: visible record index, bit 30 set when the face took the R5 clipping path */
+#define GBUF_MULTI (1 << 30)
+#define GBUF_INDEX_MASK (GBUF_MULTI - 1)
 
 typedef struct {
     int32_t A[3], B[3];
@@ -141,9 +144,12 @@ static float plane_dist(int p, const float *v, float gx, float gy)
     }
 }
 
-/* Set up face f of one frame: fills recs[0..nsub-1] (empty ones have i0>i1). Returns nsub (0 = culled). */
-static int setup_face(const float *verts, const int32_t *face3, int V, int W, int H, int f, orc_rec recs[MAX_SUB])
+/* Set up face f of one frame: fills recs[0..nsub-1] (empty ones have i0>i1). Returns nsub (0 = culled);
+ * *clipped = 1 if the face took the R5 clipping path. */
+static int setup_face(const float *verts, const int32_t *face3, int V, int W, int H, int f, orc_rec recs[MAX_SUB],
+                      int *clipped)
 {
+    *clipped = 0;
     for (int s = 0; s < MAX_SUB; ++s) { recs[s].i0 = 1; recs[s].i1 = 0; recs[s].face = f; }
     float v[3][4];
     for (int k = 0; k < 3; ++k) {
@@ -164,6 +170,7 @@ static int setup_face(const float *verts, const int32_t *face3, int V, int W, in
         return 1;
     }
     /* R5: Sutherland-Hodgman against near + 4 guard planes, carrying the parent basis */
+    *clipped = 1;
     float poly[MAX_POLY][7], tmp[MAX_POLY][7];
     int n = 3;
     for (int k = 0; k < 3; ++k) {
@@ -247,7 +254,8 @@ static inline int64_t rec_index(int F, int f, int s) { return s == 0 ? f : (int6
 
 /* ------------------------------------------------------------------------------------------------ */
 /* Setup for a whole frame: recs has 6F slots, nsub F entries */
-static int setup_frame(const float *verts, const int32_t *faces, int V, int F, int W, int H, orc_rec *recs, int32_t *nsub)
+static int setup_frame(const float *verts, const int32_t *faces, int V, int F, int W, int H, orc_rec *recs, int32_t *nsub,
+                       int32_t *clipped)
 {
     int bad = 0;
     for (int64_t i = 0; i < 6 * (int64_t)F; ++i) { recs[i].i0 = 1; recs[i].i1 = 0; recs[i].face = -1; }
@@ -256,8 +264,10 @@ static int setup_frame(const float *verts, const int32_t *faces, int V, int F, i
         const int32_t *f3 = faces + 3 * (int64_t)f;
         for (int k = 0; k < 3; ++k)
             if (f3[k] < 0 || f3[k] >= V) bad = 1;
-        int n = setup_face(verts, f3, V, W, H, f, tmp);
+        int cl = 0;
+        int n = setup_face(verts, f3, V, W, H, f, tmp, &cl);
         nsub[f] = n;
+        if (clipped) clipped[f] = cl;
         for (int s = 0; s < n; ++s) recs[rec_index(F, f, s)] = tmp[s];
     }
     return bad;
@@ -275,13 +285,14 @@ int oracle_rasterise_fwd(const float *background, const float *vertices, const f
 #endif
     orc_rec *recs = (orc_rec *)malloc(sizeof(orc_rec) * 6 * (size_t)(F > 0 ? F : 1));
     int32_t *nsub = (int32_t *)malloc(sizeof(int32_t) * (size_t)(F > 0 ? F : 1));
+    int32_t *clipped = (int32_t *)malloc(sizeof(int32_t) * (size_t)(F > 0 ? F : 1));
     uint64_t *keys = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)H * W);
     int32_t *rbuf = (int32_t *)malloc(sizeof(int32_t) * (size_t)H * W);
     for (int b = 0; b < B; ++b) {
         const float *vb = vertices + (int64_t)b * V * 4;
         const float *cb = vertex_colors + (int64_t)b * V * C;
         const int32_t *fb = faces + (int64_t)b * F * 3;
-        if (setup_frame(vb, fb, V, F, W, H, recs, nsub)) status = 2;
+        if (setup_frame(vb, fb, V, F, W, H, recs, nsub, clipped)) status = 2;
         /* raster: parallel over bands of window rows; key-min is order independent */
 #pragma omp parallel for schedule(dynamic, 1)
         for (int band = 0; band < (H + 7) / 8; ++band) {
@@ -316,7 +327,7 @@ int oracle_rasterise_fwd(const float *background, const float *vertices, const f
                     float *out = pixels + o * C;
                     const float *bg = background + o * C;
                     int32_t ri = rbuf[p];
-                    if (gbuffer) gbuffer[o] = ri;
+                    if (gbuffer) gbuffer[o] = ri < 0 ? -1 : (ri | (clipped[recs[ri].face] ? GBUF_MULTI : 0));
                     if (ri < 0) {
                         for (int c = 0; c < C; ++c) out[c] = bg[c];
                         continue;
@@ -334,7 +345,7 @@ int oracle_rasterise_fwd(const float *background, const float *vertices, const f
             }
         }
     }
-    free(recs); free(nsub); free(keys); free(rbuf);
+    free(recs); free(nsub); free(clipped); free(keys); free(rbuf);
     return status;
 }
 
@@ -402,7 +413,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
     for (int b = 0; b < B; ++b) {
         const float *vb = vertices + (int64_t)b * V * 4;
         const int32_t *fb = faces + (int64_t)b * F * 3;
-        if (setup_frame(vb, fb, V, F, W, H, recs, nsub)) status = 2;
+        if (setup_frame(vb, fb, V, F, W, H, recs, nsub, NULL)) status = 2;
         memset(accv, 0, sizeof(double) * (size_t)nthr * V * 4);
         memset(accc, 0, sizeof(double) * (size_t)nthr * V * C);
 #pragma omp parallel
@@ -418,7 +429,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
                     int row = H - 1 - j;
                     int64_t o = ((int64_t)b * H + row) * W + i;
                     const float *G = grad_pixels + o * C, *I = pixels + o * C;
-                    int32_t rp = gbuffer[o];
+                    int32_t rp = gbuffer[o] < 0 ? -1 : (gbuffer[o] & GBUF_INDEX_MASK);
                     float *gbg = grad_background + o * C;
                     if (rp < 0) {
                         for (int c = 0; c < C; ++c) gbg[c] = G[c];
@@ -438,7 +449,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
                         int i2 = i + (axis == 0), j2 = j + (axis == 1);
                         if (i2 >= W || j2 >= H) continue;
                         int64_t o2 = ((int64_t)b * H + (H - 1 - j2)) * W + i2;
-                        int32_t rq = gbuffer[o2];
+                        int32_t rq = gbuffer[o2] < 0 ? -1 : (gbuffer[o2] & GBUF_INDEX_MASK);
                         if (rp < 0 && rq < 0) continue;
                         const float *G2 = grad_pixels + o2 * C, *I2 = pixels + o2 * C;
                         float acc = 0.0f;
