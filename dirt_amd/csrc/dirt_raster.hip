@@ -524,11 +524,11 @@ __device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_
         for (int k = 0; k < 3; ++k)
             small = small && R.A[k] > -kSmallEdge && R.A[k] < kSmallEdge && R.B[k] > -kSmallEdge && R.B[k] < kSmallEdge;
         keep = true;
-        const int64_t px0 = (int64_t)si0 * 256 + 128, py0 = (int64_t)sj0 * 256 + 128;
+        const int32_t px0 = si0 * 256 + 128, py0 = sj0 * 256 + 128;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
-            const int64_t e0 = (int64_t)R.A[k] * px0 + (int64_t)R.B[k] * py0 + R.C[k] + owned;
+            const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
             const int64_t sx = (int64_t)R.A[k] * (15 * 256), sy = (int64_t)R.B[k] * (3 * 256);
             const int64_t emin = e0 + (sx < 0 ? sx : 0) + (sy < 0 ? sy : 0);
             const int64_t emax = e0 + (sx > 0 ? sx : 0) + (sy > 0 ? sy : 0);
@@ -706,17 +706,16 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 // sub-records of f are only consulted when f was clipped into several (`multi`).
 __device__ __forceinline__ bool edge_covers(const EdgePart &r, int i, int j)
 {
+    // empty records have i0 > i1 and are rejected by the bbox test
     if (r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1) return false;
     int64_t E[3];
     edge_values(r, i, j, E);
     return inside(r, E);
 }
 
-__device__ bool covers_face(const EdgePart &hint, int64_t hint_ri, bool multi, const Rec *frame_recs,
-                            const FaceData *fdata_frame, int F, int f, int i, int j)
+__device__ __noinline__ bool covers_face_multi(int64_t hint_ri, const Rec *frame_recs, const FaceData *fdata_frame,
+                                               int F, int f, int i, int j)
 {
-    if (edge_covers(hint, i, j)) return true;
-    if (!multi) return false;
     const int n = fdata_frame[f].nsub;
     for (int s = 0; s < n; ++s) {
         const int64_t ri = rec_index(F, f, s);
@@ -724,6 +723,14 @@ __device__ bool covers_face(const EdgePart &hint, int64_t hint_ri, bool multi, c
         if (edge_covers(*reinterpret_cast<const EdgePart *>(&frame_recs[ri]), i, j)) return true;
     }
     return false;
+}
+
+__device__ __forceinline__ bool covers_face(const EdgePart &hint, int64_t hint_ri, bool multi, const Rec *frame_recs,
+                            const FaceData *fdata_frame, int F, int f, int i, int j)
+{
+    if (edge_covers(hint, i, j)) return true;
+    if (!multi) return false;
+    return covers_face_multi(hint_ri, frame_recs, fdata_frame, F, f, i, j);
 }
 
 template <int D>
@@ -767,9 +774,70 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
 }
 
 constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
-constexpr int kHashSlots = 256;    // >= distinct records a 256-pixel tile can hold
+constexpr int kHaloPix = kHalo * kHalo;
+constexpr int kSlots = 128;        // distinct records per tile+halo kept in LDS (typ. 10-40)
+constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
 
-template <int CC>
+// LDS-resident view of one setup record: what coverage tests and interpolation need
+struct SlotTable {
+    int32_t key[kSlots];     // g-buffer word (record index | clipped flag), -1 = free
+    int32_t list[kSlots];    // occupied slots in insertion order
+    int32_t A[3][kSlots], B[3][kSlots];
+    int64_t C[3][kSlots];
+    uint32_t bx[kSlots], by[kSlots];
+    float iw[3][kSlots], w[3][kSlots];
+    int32_t v[3][kSlots];
+    int32_t n;
+};
+
+struct RecRegs {  // one record in registers
+    EdgePart e;
+    float iw[3], w[3];
+};
+
+__device__ __forceinline__ void load_slot(const SlotTable &T, int s, RecRegs &R)
+{
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        R.e.A[k] = T.A[k][s]; R.e.B[k] = T.B[k][s]; R.e.C[k] = T.C[k][s];
+        R.iw[k] = T.iw[k][s]; R.w[k] = T.w[k][s];
+    }
+    R.e.i0 = (uint16_t)(T.bx[s] & 0xffff); R.e.i1 = (uint16_t)(T.bx[s] >> 16);
+    R.e.j0 = (uint16_t)(T.by[s] & 0xffff); R.e.j1 = (uint16_t)(T.by[s] >> 16);
+}
+
+__device__ __forceinline__ void load_global(const Rec *frame_recs, const FaceData *fdata_frame, int F, int32_t ri,
+                                            RecRegs &R)
+{
+    const Rec &r = frame_recs[ri];
+    R.e = *reinterpret_cast<const EdgePart *>(&r);
+    const FaceData &fd = fdata_frame[face_of_record(ri, F)];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { R.iw[k] = r.iw[k]; R.w[k] = fd.w[k]; }
+}
+
+__device__ __forceinline__ int slot_hash(int32_t key) { return (int)(((uint32_t)key * 2654435761u) >> 25) & (kSlots - 1); }
+
+// insert `key`, return its slot or kNoSlot if the table is full
+__device__ __forceinline__ int slot_insert(SlotTable &T, int32_t key)
+{
+    int slot = slot_hash(key);
+    for (int probe = 0; probe < kSlots; ++probe) {
+        const int old = atomicCAS(&T.key[slot], -1, key);
+        if (old == -1) {
+            T.list[atomicAdd(&T.n, 1)] = slot;
+            return slot;
+        }
+        if (old == key) return slot;
+        slot = (slot + 1) & (kSlots - 1);
+    }
+    return kNoSlot;
+}
+
+// AB: ablation mask for tools/ablate.py (0 in the product): 1 skip pairs, 2 skip colour weights,
+// 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
+// 32 skip the DPP run scan (every lane adds into LDS), 64 skip the LDS adds of the run tails
+template <int CC, int AB = 0>
 __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
@@ -780,14 +848,12 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     constexpr int NVM = 9 + 3 * CM;
     const int C = CC > 0 ? CC : Cdyn;
     const int NV = 9 + 3 * C;
-    __shared__ int32_t s_rec[kHalo * kHalo];
-    __shared__ float s_G[kHalo * kHalo * CM];
-    __shared__ float s_I[kHalo * kHalo * CM];
-    __shared__ int32_t s_keys[kHashSlots];
-    __shared__ int32_t s_list[kHashSlots];
-    __shared__ int32_t s_vid[kHashSlots * 3];
-    __shared__ float s_vals[kHashSlots * NVM];
-    __shared__ int32_t s_n;
+    __shared__ int32_t s_gb[kHaloPix];
+    __shared__ int32_t s_slot[kHaloPix];
+    __shared__ float s_G[kHaloPix * CM];
+    __shared__ float s_I[kHaloPix * CM];
+    __shared__ SlotTable T;
+    __shared__ float s_vals[kSlots * NVM];
 
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
@@ -797,29 +863,60 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
     const float inv_hw = 2.0f / (float)W, inv_hh = 2.0f / (float)H;
 
-    for (int k = t; k < kHashSlots; k += 256) s_keys[k] = -1;
-    for (int k = t; k < kHashSlots * NVM; k += 256) s_vals[k] = 0.0f;
-    if (t == 0) s_n = 0;
-    // stage gbuffer / G / I of the tile plus a one-pixel halo (window coords, j from the bottom)
+    // ---- phase A: stage g-buffer / G / I of the tile + one-pixel halo, build the slot table
+    for (int k = t; k < kSlots; k += 256) T.key[k] = -1;
+    for (int k = t; k < kSlots * NVM; k += 256) s_vals[k] = 0.0f;
+    if (t == 0) T.n = 0;
     const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
-    for (int k = t; k < kHalo * kHalo; k += 256) {
+    for (int k = t; k < kHaloPix; k += 256) {
         const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
         if (hi < 0 || hj < 0 || hi >= W || hj >= H) {
-            s_rec[k] = -2;
+            s_gb[k] = -2;
             continue;
         }
         const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
-        s_rec[k] = gbuffer[o];
+        s_gb[k] = gbuffer[o];
         for (int c = 0; c < C; ++c) {
             s_G[k * CM + c] = grad_pixels[o * C + c];
             s_I[k * CM + c] = pixels[o * C + c];
         }
     }
     __syncthreads();
-
-    const bool in_frame = i < W && j < H;
     const int kme = (ly + 1) * kHalo + (lx + 1);
-    const int32_t gp = in_frame ? s_rec[kme] : -2;
+    {
+        // own pixels first (<= 256 distinct keys may not all fit: the rest read global memory),
+        // then the halo ring
+        const int32_t g = s_gb[kme];
+        s_slot[kme] = g >= 0 ? slot_insert(T, g) : -1;
+    }
+    __syncthreads();
+    for (int k = t; k < kHaloPix; k += 256) {
+        const int hx = k % kHalo, hy = k / kHalo;
+        if (hx != 0 && hy != 0 && hx != kHalo - 1 && hy != kHalo - 1) continue;
+        const int32_t g = s_gb[k];
+        s_slot[k] = g >= 0 ? slot_insert(T, g) : -1;
+    }
+    __syncthreads();
+    const int nslots = T.n;
+    for (int e = t; e < nslots; e += 256) {
+        const int s = T.list[e];
+        const int32_t ri = T.key[s] & kGbufIndexMask;
+        const Rec &r = frame_recs[ri];
+        const EdgePart ep = *reinterpret_cast<const EdgePart *>(&r);
+        const FaceData fd = fdata_frame[face_of_record(ri, F)];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k]; T.C[k][s] = ep.C[k];
+            T.iw[k][s] = r.iw[k]; T.w[k][s] = fd.w[k]; T.v[k][s] = fd.v[k];
+        }
+        T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16);
+        T.by[s] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
+    }
+    __syncthreads();
+
+    // ---- phase B: per-pixel contributions to the face visible at this pixel
+    const bool in_frame = i < W && j < H;
+    const int32_t gp = in_frame ? s_gb[kme] : -2;
     const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
     if (in_frame) {
         const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
@@ -829,38 +926,24 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     float acc[NVM];
 #pragma unroll
     for (int v = 0; v < NVM; ++v) acc[v] = 0.0f;
-    int key = -1;
-    FaceData fd;
+    const int sp = rp >= 0 ? s_slot[kme] : -1;
     if (rp >= 0) {
-        // Every global load this lane needs is issued up front: the own record's edges, 1/w and (only
-        // for clipped faces) basis, the face data, and the edge part of each neighbour's record where
-        // the neighbour shows a different face.  Ownership decisions (covers tests) are exact int64;
-        // the interpolation weights use fast reciprocals (contributions agree with the oracle to
-        // ~1e-6 relative, far inside the 1e-4 tolerance the atomic summation order already needs).
+        // Ownership decisions (coverage tests) are exact int64; the interpolation weights use fast
+        // reciprocals (contributions agree with the oracle to ~1e-6 relative, far inside the 1e-4
+        // tolerance the atomic summation order already needs).
         const int f = face_of_record(rp, F);
         const bool multi = (gp & kGbufMulti) != 0;
-        const Rec &rr = frame_recs[rp];
-        const EdgePart mine = *reinterpret_cast<const EdgePart *>(&rr);
-        const float iw0 = rr.iw[0], iw1 = rr.iw[1], iw2 = rr.iw[2];
-        fd = fdata_frame[f];
-        int32_t gq[4], fqv[4];
-        EdgePart nb[4];
-#pragma unroll
-        for (int dir = 0; dir < 4; ++dir) {
-            const int axis = dir >> 1, sgn = (dir & 1) ? -1 : 1;
-            const int kq = kme + (axis == 1 ? sgn * kHalo : 0) + (axis == 0 ? sgn : 0);
-            gq[dir] = s_rec[kq];
-            fqv[dir] = gq[dir] >= 0 ? face_of_record(gq[dir] & kGbufIndexMask, F) : -1;
-            if (fqv[dir] >= 0 && fqv[dir] != f)
-                nb[dir] = *reinterpret_cast<const EdgePart *>(&frame_recs[gq[dir] & kGbufIndexMask]);
-        }
+        RecRegs me;
+        if (sp >= 0) load_slot(T, sp, me);
+        else load_global(frame_recs, fdata_frame, F, rp, me);
         int64_t Ep[3];
-        edge_values(mine, i, j, Ep);
+        edge_values(me.e, i, j, Ep);
         float fEp[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) fEp[k] = fast_i64_to_f32(Ep[k]);
+        const Rec &rr = frame_recs[rp];  // basis is only read for clipped faces
         float lam[3];
-        if (fast_lambda(rr, multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
+        if (!(AB & 2) && fast_lambda(rr, multi, fEp[0] * me.iw[0], fEp[1] * me.iw[1], fEp[2] * me.iw[2], lam)) {
 #pragma unroll
             for (int k = 0; k < 3; ++k)
                 for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * s_G[kme * CM + c];
@@ -868,11 +951,13 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window)
 #pragma unroll
         for (int dir = 0; dir < 4; ++dir) {
+            if (AB & 1) break;
             const int axis = dir >> 1;
             const bool me_low = (dir & 1) == 0;
             const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
             const int kq = kme + dj * kHalo + di;
-            if (gq[dir] == -2) continue;
+            const int32_t gq = s_gb[kq];
+            if (gq == -2) continue;
             const int klo = me_low ? kme : kq, kup = me_low ? kq : kme;
             float a = 0.0f;
             for (int c = 0; c < C; ++c)
@@ -880,36 +965,49 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             const float s = -0.5f * a;
             if (s == 0.0f) continue;
             const int iq = i + di, jq = j + dj;
-            const int fq = fqv[dir];
+            const int32_t rq = gq >= 0 ? (gq & kGbufIndexMask) : -1;
+            const int fq = rq >= 0 ? face_of_record(rq, F) : -1;
             // exact edge values of this face at the neighbour: one step of 256 sub-pixels
             int64_t step[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) step[k] = (int64_t)(axis == 0 ? mine.A[k] : mine.B[k]) * (me_low ? 256 : -256);
+            for (int k = 0; k < 3; ++k) step[k] = (int64_t)(axis == 0 ? me.e.A[k] : me.e.B[k]) * (me_low ? 256 : -256);
             float omega;
             if (fq == f) {
                 omega = me_low ? 1.0f : 0.0f;
             } else if (fq < 0) {
                 omega = 1.0f;
+            } else if (AB & 16) {
+                omega = 0.5f;
             } else {
                 int64_t Eq[3];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) Eq[k] = Ep[k] + step[k];
-                bool mine_covers_other = inside(mine, Eq);
+                bool mine_covers_other = inside(me.e, Eq);
                 if (!mine_covers_other && multi)
-                    mine_covers_other = covers_face(mine, rp, true, frame_recs, fdata_frame, F, f, iq, jq);
-                const bool other_covers_me = covers_face(nb[dir], gq[dir] & kGbufIndexMask, (gq[dir] & kGbufMulti) != 0,
-                                                         frame_recs, fdata_frame, F, fq, i, j);
+                    mine_covers_other = covers_face_multi(rp, frame_recs, fdata_frame, F, f, iq, jq);
+                const int sq = s_slot[kq];
+                EdgePart other;
+                if (sq >= 0) {
+                    RecRegs o;
+                    load_slot(T, sq, o);
+                    other = o.e;
+                } else {
+                    other = *reinterpret_cast<const EdgePart *>(&frame_recs[rq]);
+                }
+                bool other_covers_me = edge_covers(other, i, j);
+                if (!other_covers_me && (gq & kGbufMulti))
+                    other_covers_me = covers_face_multi(rq, frame_recs, fdata_frame, F, fq, i, j);
                 omega = (!mine_covers_other && other_covers_me) ? 1.0f
                         : (mine_covers_other && !other_covers_me) ? 0.0f : 0.5f;
             }
             if (omega == 0.0f) continue;
             // midpoint: E(p) + E(q) = 2 E(p) + step
-            const float m0 = (2.0f * fEp[0] + (float)step[0]) * iw0;
-            const float m1 = (2.0f * fEp[1] + (float)step[1]) * iw1;
-            const float m2 = (2.0f * fEp[2] + (float)step[2]) * iw2;
+            const float m0 = (2.0f * fEp[0] + (float)step[0]) * me.iw[0];
+            const float m1 = (2.0f * fEp[1] + (float)step[1]) * me.iw[1];
+            const float m2 = (2.0f * fEp[2] + (float)step[2]) * me.iw[2];
             float lm[3];
             if (!fast_lambda(rr, multi, m0, m1, m2, lm)) continue;
-            const float Wm = (lm[0] * fd.w[0] + lm[1] * fd.w[1]) + lm[2] * fd.w[2];
+            const float Wm = (lm[0] * me.w[0] + lm[1] * me.w[1]) + lm[2] * me.w[2];
             if (Wm == 0.0f) continue;
             const int ilo = me_low ? i : iq, jlo = me_low ? j : jq;
             const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
@@ -923,10 +1021,18 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
                 acc[k * 3 + 2] -= g * ndc;
             }
         }
-        key = rp;
+    }
+    if (AB & 4) {
+        float z = 0.0f;
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) z += acc[v];
+        if (z == 1234.5f) grad_verts[t] = z;  // keep the contributions live
+        return;
     }
 
-    // 1. segmented sum over runs of equal key along the 16-lane row
+    // ---- phase C: segmented sum over runs of equal key along each 16-lane row (one DPP row),
+    // then the run tails add into the LDS slot accumulators (or global atomics without a slot)
+    const int key = rp >= 0 ? rp : -1;
     const int kl = dpp_shr_i<1>(key, -3);
     int start = (lx == 0 || kl != key) ? lx : -1;
     start = max(start, dpp_shr_i<1>(start, -1));
@@ -935,6 +1041,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     start = max(start, dpp_shr_i<8>(start, -1));
 #pragma unroll
     for (int v = 0; v < NVM; ++v) {
+        if (AB & 32) break;
         float x = acc[v];
         float y;
         y = dpp_shr_f<1>(x); if (lx - 1 >= start) x += y;
@@ -944,40 +1051,35 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         acc[v] = x;
     }
     const int kr = dpp_shl_i<1>(key, -3);
-    const bool tail = key >= 0 && (lx == 15 || kr != key);
-
-    // 2. run tails accumulate into the tile's LDS hash table
+    const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key) && !(AB & 64);
+    float *gvb = grad_verts + (int64_t)b * V * 4;
+    float *gcb = grad_colors + (int64_t)b * V * C;
     if (tail) {
-        int slot = (int)(((uint32_t)key * 2654435761u) >> 24) & (kHashSlots - 1);
-        while (true) {
-            const int old = atomicCAS(&s_keys[slot], -1, key);
-            if (old == -1) {
-                s_list[atomicAdd(&s_n, 1)] = slot;
-                s_vid[slot * 3 + 0] = fd.v[0];
-                s_vid[slot * 3 + 1] = fd.v[1];
-                s_vid[slot * 3 + 2] = fd.v[2];
-                break;
+        if (sp >= 0) {
+#pragma unroll
+            for (int v = 0; v < NVM; ++v)
+                if (v < NV) atomicAdd(&s_vals[sp * NVM + v], acc[v]);
+        } else {
+            const FaceData &fd = fdata_frame[face_of_record(rp, F)];
+            for (int v = 0; v < NV; ++v) {
+                if (acc[v] == 0.0f) continue;
+                if (v < 9) atomicAdd(gvb + (int64_t)fd.v[v / 3] * 4 + ((v % 3) == 2 ? 3 : v % 3), acc[v]);
+                else atomicAdd(gcb + (int64_t)fd.v[(v - 9) / C] * C + (v - 9) % C, acc[v]);
             }
-            if (old == key) break;
-            slot = (slot + 1) & (kHashSlots - 1);
         }
-        for (int v = 0; v < NV; ++v)
-            if (acc[v] != 0.0f) atomicAdd(&s_vals[slot * NVM + v], acc[v]);
     }
     __syncthreads();
 
-    // 3. flush: one wave-instruction of global atomics per (tile, record)
-    const int n = s_n, wave = t >> 6, lane = t & 63;
-    float *gvb = grad_verts + (int64_t)b * V * 4;
-    float *gcb = grad_colors + (int64_t)b * V * C;
+    // ---- phase D: flush, one wave-instruction of global atomics per (tile, record) with data
+    const int n = (AB & 8) ? 0 : nslots, wave = t >> 6, lane = t & 63;
     if (lane < NV) {
         const int k = lane < 9 ? lane / 3 : (lane - 9) / C;
         const int comp = lane < 9 ? ((lane % 3) == 2 ? 3 : lane % 3) : (lane - 9) % C;
         for (int e = wave; e < n; e += 4) {
-            const int slot = s_list[e];
+            const int slot = T.list[e];
             const float val = s_vals[slot * NVM + lane];
             if (val == 0.0f) continue;
-            const int vtx = s_vid[slot * 3 + k];
+            const int vtx = T.v[k][slot];
             if (lane < 9) atomicAdd(gvb + (int64_t)vtx * 4 + comp, val);
             else atomicAdd(gcb + (int64_t)vtx * C + comp, val);
         }
@@ -1115,6 +1217,49 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     else LAUNCH_GRAD(0);
 #undef LAUNCH_GRAD
     HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+// Ablation entry point (tools/ablate.py): the backward with parts of grad_kernel switched off.
+// Not part of include/dirt_mi355x.h; C == 3 only.  Returns the kernel time in ms (hipEvents).
+int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
+                           const void *saved, int B, int H, int W, int C, int V, int F, float *grad_vertices,
+                           float *grad_vertex_colors, float *grad_background, void *stream_, float *ms)
+{
+    if (C != 3) return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: C must be 3");
+    Layout L;
+    int rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const char *sv = static_cast<const char *>(saved);
+    const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
+    const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)B * V * 4 * sizeof(float), stream));
+    HIP_TRY(hipMemsetAsync(grad_vertex_colors, 0, (size_t)B * V * C * sizeof(float), stream));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, stream));
+    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+#define V_GRAD(AB)                                                                                                   \
+    case AB:                                                                                                         \
+        grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, recs, fdata, B, H, W, C, V, \
+                                                           F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,     \
+                                                           grad_background);                                         \
+        break
+    switch (variant) {
+        V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);
+        V_GRAD(32); V_GRAD(64); V_GRAD(72);
+    default:
+        return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: unknown variant");
+    }
+#undef V_GRAD
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    HIP_TRY(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return DIRT_OK;
 }
 

@@ -145,23 +145,24 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
 }
 
 // R3: exact edge values at pixel centre (i,j)
+// (32 x 32 -> 64-bit signed multiplies: one v_mad_i64_i32 each; pixel coordinates fit in 22 bits)
 template <typename R>
 __device__ __forceinline__ void edge_values(const R &r, int i, int j, int64_t E[3])
 {
-    const int64_t px = (int64_t)i * 256 + 128, py = (int64_t)j * 256 + 128;
+    const int32_t px = i * 256 + 128, py = j * 256 + 128;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) E[k] = (int64_t)r.A[k] * px + (int64_t)r.B[k] * py + r.C[k];
+    for (int k = 0; k < 3; ++k) E[k] = (int64_t)r.A[k] * (int64_t)px + ((int64_t)r.B[k] * (int64_t)py + r.C[k]);
 }
 
-// R3 top-left rule
+// R3 top-left rule: E > 0, or E == 0 on an owned (left or top) edge  <=>  E + owned > 0
 template <typename R>
 __device__ __forceinline__ bool inside(const R &r, const int64_t E[3])
 {
     bool in = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const bool owned = r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0);
-        in = in && (E[k] > 0 || (E[k] == 0 && owned));
+        const int64_t owned = (r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0)) ? 1 : 0;
+        in = in && (E[k] + owned > 0);
     }
     return in;
 }

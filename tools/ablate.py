@@ -1,0 +1,49 @@
+"""Interleaved A/B timing of grad_kernel ablation variants (one process, median of N rounds)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+import scenes  # noqa: E402
+from dirt_amd import _lib  # noqa: E402
+from dirt_amd.session import RasteriseSession  # noqa: E402
+
+NAMES = {0: "full", 1: "no pairs", 2: "no colour", 3: "no pairs+colour", 4: "no reduction", 5: "no pairs+reduction",
+         7: "nothing but staging", 8: "no flush", 16: "no coverage tests", 32: "no DPP scan (all lanes add)",
+         64: "no LDS adds", 72: "no LDS adds, no flush"}
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    bg, v, c, f = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
+    t = [torch.from_numpy(a[None]).to(dev) for a in (bg, v, c, f)]
+    B, H, W, C = t[0].shape
+    V, F = t[1].shape[1], t[3].shape[1]
+    sess = RasteriseSession(B, H, W, C, V, F, device=dev)
+    sess.forward(*t)
+    g = torch.randn_like(sess.pixels)
+    lib = _lib.load()
+    fn = lib.dirt_debug_bwd_variant
+    P = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_int, P, P, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, ctypes.POINTER(ctypes.c_float)]
+    fn.restype = ctypes.c_int
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {k: [] for k in NAMES}
+    ms = ctypes.c_float(0)
+    for rnd in range(30):
+        for k in NAMES:
+            _lib.check(fn(k, sess.pixels.data_ptr(), g.data_ptr(), sess.gbuffer.data_ptr(), sess.saved.data_ptr(),
+                          B, H, W, C, V, F, sess.grad_vertices.data_ptr(), sess.grad_vertex_colors.data_ptr(),
+                          sess.grad_background.data_ptr(), stream, ctypes.byref(ms)))
+            if rnd >= 3:
+                res[k].append(ms.value * 1e3)
+    for k, name in NAMES.items():
+        print("%-22s median %8.2f us  min %8.2f" % (name, np.median(res[k]), np.min(res[k])))
+
+
+if __name__ == "__main__":
+    main()
