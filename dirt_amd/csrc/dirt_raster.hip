@@ -778,42 +778,24 @@ constexpr int kHaloPix = kHalo * kHalo;
 constexpr int kSlots = 128;        // distinct records per tile+halo kept in LDS (typ. 10-40)
 constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
 
-// LDS-resident view of one setup record: what coverage tests and interpolation need
+// LDS-resident copy of the edge part of the records seen in a tile + halo (for coverage tests of a
+// neighbour's face) and of their vertex ids (for the flush).
 struct SlotTable {
     int32_t key[kSlots];     // g-buffer word (record index | clipped flag), -1 = free
     int32_t list[kSlots];    // occupied slots in insertion order
     int32_t A[3][kSlots], B[3][kSlots];
     int64_t C[3][kSlots];
     uint32_t bx[kSlots], by[kSlots];
-    float iw[3][kSlots], w[3][kSlots];
     int32_t v[3][kSlots];
     int32_t n;
 };
 
-struct RecRegs {  // one record in registers
-    EdgePart e;
-    float iw[3], w[3];
-};
-
-__device__ __forceinline__ void load_slot(const SlotTable &T, int s, RecRegs &R)
+__device__ __forceinline__ void load_slot_edges(const SlotTable &T, int s, EdgePart &e)
 {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        R.e.A[k] = T.A[k][s]; R.e.B[k] = T.B[k][s]; R.e.C[k] = T.C[k][s];
-        R.iw[k] = T.iw[k][s]; R.w[k] = T.w[k][s];
-    }
-    R.e.i0 = (uint16_t)(T.bx[s] & 0xffff); R.e.i1 = (uint16_t)(T.bx[s] >> 16);
-    R.e.j0 = (uint16_t)(T.by[s] & 0xffff); R.e.j1 = (uint16_t)(T.by[s] >> 16);
-}
-
-__device__ __forceinline__ void load_global(const Rec *frame_recs, const FaceData *fdata_frame, int F, int32_t ri,
-                                            RecRegs &R)
-{
-    const Rec &r = frame_recs[ri];
-    R.e = *reinterpret_cast<const EdgePart *>(&r);
-    const FaceData &fd = fdata_frame[face_of_record(ri, F)];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { R.iw[k] = r.iw[k]; R.w[k] = fd.w[k]; }
+    for (int k = 0; k < 3; ++k) { e.A[k] = T.A[k][s]; e.B[k] = T.B[k][s]; e.C[k] = T.C[k][s]; }
+    e.i0 = (uint16_t)(T.bx[s] & 0xffff); e.i1 = (uint16_t)(T.bx[s] >> 16);
+    e.j0 = (uint16_t)(T.by[s] & 0xffff); e.j1 = (uint16_t)(T.by[s] >> 16);
 }
 
 __device__ __forceinline__ int slot_hash(int32_t key) { return (int)(((uint32_t)key * 2654435761u) >> 25) & (kSlots - 1); }
@@ -834,9 +816,21 @@ __device__ __forceinline__ int slot_insert(SlotTable &T, int32_t key)
     return kNoSlot;
 }
 
+// Index (0..15) of the first lane of this lane's run of equal `key` in its 16-lane DPP row.
+__device__ __forceinline__ int run_start(int key, int lx)
+{
+    const int kl = dpp_shr_i<1>(key, -3);
+    int start = (lx == 0 || kl != key) ? lx : -1;
+    start = max(start, dpp_shr_i<1>(start, -1));
+    start = max(start, dpp_shr_i<2>(start, -1));
+    start = max(start, dpp_shr_i<4>(start, -1));
+    start = max(start, dpp_shr_i<8>(start, -1));
+    return start;
+}
+
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip pairs, 2 skip colour weights,
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
-// 32 skip the DPP run scan (every lane adds into LDS), 64 skip the LDS adds of the run tails
+// 32 skip the DPP run scan (every lane adds into LDS)
 template <int CC, int AB = 0>
 __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
@@ -845,15 +839,20 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
                                                    float *__restrict__ grad_colors, float *__restrict__ grad_bg)
 {
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
+    constexpr int CP = CM == 3 ? 4 : CM;  // LDS pixel stride (float4 for RGB)
     constexpr int NVM = 9 + 3 * CM;
     const int C = CC > 0 ? CC : Cdyn;
     const int NV = 9 + 3 * C;
     __shared__ int32_t s_gb[kHaloPix];
     __shared__ int32_t s_slot[kHaloPix];
-    __shared__ float s_G[kHaloPix * CM];
-    __shared__ float s_I[kHaloPix * CM];
+    __shared__ float s_sx[kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), see DESIGN.md 4
+    __shared__ float s_sy[kHaloPix];
+    __shared__ __attribute__((aligned(16))) float s_G[kHaloPix * CP];
+    __shared__ __attribute__((aligned(16))) float s_I[kHaloPix * CP];
     __shared__ SlotTable T;
-    __shared__ float s_vals[kSlots * NVM];
+    __shared__ float s_part[256 * NVM];  // run-tail partial sums, indexed by thread id
+    __shared__ int32_t s_head[kSlots];   // per slot: linked list of its run tails
+    __shared__ int32_t s_next[256];
 
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
@@ -862,10 +861,14 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
     const float inv_hw = 2.0f / (float)W, inv_hh = 2.0f / (float)H;
+    const int kme = (ly + 1) * kHalo + (lx + 1);
+    const bool in_frame = i < W && j < H;
 
-    // ---- phase A: stage g-buffer / G / I of the tile + one-pixel halo, build the slot table
-    for (int k = t; k < kSlots; k += 256) T.key[k] = -1;
-    for (int k = t; k < kSlots * NVM; k += 256) s_vals[k] = 0.0f;
+    // ---- phase A: stage g-buffer / G / I of the tile + one-pixel halo, pair scalars, slot table
+    for (int k = t; k < kSlots; k += 256) {
+        T.key[k] = -1;
+        s_head[k] = -1;
+    }
     if (t == 0) T.n = 0;
     const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
     for (int k = t; k < kHaloPix; k += 256) {
@@ -876,18 +879,50 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         }
         const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
         s_gb[k] = gbuffer[o];
-        for (int c = 0; c < C; ++c) {
-            s_G[k * CM + c] = grad_pixels[o * C + c];
-            s_I[k * CM + c] = pixels[o * C + c];
+        if (CP == 4 && C == 3) {
+            const float *gp = grad_pixels + o * 3, *ip = pixels + o * 3;
+            *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(gp[0], gp[1], gp[2], 0.0f);
+            *reinterpret_cast<float4 *>(&s_I[k * CP]) = make_float4(ip[0], ip[1], ip[2], 0.0f);
+        } else {
+            for (int c = 0; c < C; ++c) {
+                s_G[k * CP + c] = grad_pixels[o * C + c];
+                s_I[k * CP + c] = pixels[o * C + c];
+            }
         }
     }
     __syncthreads();
-    const int kme = (ly + 1) * kHalo + (lx + 1);
+    const int32_t gp = in_frame ? s_gb[kme] : -2;
     {
-        // own pixels first (<= 256 distinct keys may not all fit: the rest read global memory),
-        // then the halo ring
+        // pair scalars for pairs starting at a staged pixel (same operand order as the oracle)
+        for (int k = t; k < kHaloPix; k += 256) {
+            const int hx = k % kHalo, hy = k / kHalo;
+            float sx = 0.0f, sy = 0.0f;
+            if (s_gb[k] != -2) {
+                if (hx + 1 < kHalo && s_gb[k + 1] != -2) {
+                    float a = 0.0f;
+                    for (int c = 0; c < C; ++c)
+                        a += (s_G[k * CP + c] + s_G[(k + 1) * CP + c]) * (s_I[(k + 1) * CP + c] - s_I[k * CP + c]);
+                    sx = -0.5f * a;
+                }
+                if (hy + 1 < kHalo && s_gb[k + kHalo] != -2) {
+                    float a = 0.0f;
+                    for (int c = 0; c < C; ++c)
+                        a += (s_G[k * CP + c] + s_G[(k + kHalo) * CP + c]) * (s_I[(k + kHalo) * CP + c] - s_I[k * CP + c]);
+                    sy = -0.5f * a;
+                }
+            }
+            s_sx[k] = sx;
+            s_sy[k] = sy;
+        }
+        // own pixels first (run heads only; all 256 distinct keys may not fit: the rest read global
+        // memory), then the halo ring
         const int32_t g = s_gb[kme];
-        s_slot[kme] = g >= 0 ? slot_insert(T, g) : -1;
+        const int key = g >= 0 ? g : -1;
+        const int start = run_start(key, lx);
+        int slot = -1;
+        if (key >= 0 && start == lx) slot = slot_insert(T, key);
+        slot = __shfl(slot, (t & 48) + start, 64);
+        s_slot[kme] = key >= 0 ? slot : -1;
     }
     __syncthreads();
     for (int k = t; k < kHaloPix; k += 256) {
@@ -901,13 +936,12 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     for (int e = t; e < nslots; e += 256) {
         const int s = T.list[e];
         const int32_t ri = T.key[s] & kGbufIndexMask;
-        const Rec &r = frame_recs[ri];
-        const EdgePart ep = *reinterpret_cast<const EdgePart *>(&r);
-        const FaceData fd = fdata_frame[face_of_record(ri, F)];
+        const EdgePart ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
+        const FaceData &fd = fdata_frame[face_of_record(ri, F)];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k]; T.C[k][s] = ep.C[k];
-            T.iw[k][s] = r.iw[k]; T.w[k][s] = fd.w[k]; T.v[k][s] = fd.v[k];
+            T.v[k][s] = fd.v[k];
         }
         T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16);
         T.by[s] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
@@ -915,12 +949,10 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     __syncthreads();
 
     // ---- phase B: per-pixel contributions to the face visible at this pixel
-    const bool in_frame = i < W && j < H;
-    const int32_t gp = in_frame ? s_gb[kme] : -2;
     const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
     if (in_frame) {
         const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
-        for (int c = 0; c < C; ++c) grad_bg[o * C + c] = rp < 0 ? s_G[kme * CM + c] : 0.0f;
+        for (int c = 0; c < C; ++c) grad_bg[o * C + c] = rp < 0 ? s_G[kme * CP + c] : 0.0f;
     }
 
     float acc[NVM];
@@ -930,23 +962,28 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     if (rp >= 0) {
         // Ownership decisions (coverage tests) are exact int64; the interpolation weights use fast
         // reciprocals (contributions agree with the oracle to ~1e-6 relative, far inside the 1e-4
-        // tolerance the atomic summation order already needs).
+        // tolerance the atomic summation order already needs).  The own record comes through the
+        // vector-memory path (L1-resident: a wave touches a handful of records).
         const int f = face_of_record(rp, F);
         const bool multi = (gp & kGbufMulti) != 0;
-        RecRegs me;
-        if (sp >= 0) load_slot(T, sp, me);
-        else load_global(frame_recs, fdata_frame, F, rp, me);
+        const Rec &rr = frame_recs[rp];
+        const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+        const float iw0 = rr.iw[0], iw1 = rr.iw[1], iw2 = rr.iw[2];
+        const FaceData &fdr = fdata_frame[f];
+        const float w0 = fdr.w[0], w1 = fdr.w[1], w2 = fdr.w[2];
         int64_t Ep[3];
-        edge_values(me.e, i, j, Ep);
+        edge_values(me, i, j, Ep);
         float fEp[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) fEp[k] = fast_i64_to_f32(Ep[k]);
-        const Rec &rr = frame_recs[rp];  // basis is only read for clipped faces
         float lam[3];
-        if (!(AB & 2) && fast_lambda(rr, multi, fEp[0] * me.iw[0], fEp[1] * me.iw[1], fEp[2] * me.iw[2], lam)) {
+        if (!(AB & 2) && fast_lambda(rr, multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
+            float Gm[CM];
+#pragma unroll
+            for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * s_G[kme * CM + c];
+                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * Gm[c];
         }
         // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window)
 #pragma unroll
@@ -958,11 +995,8 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             const int kq = kme + dj * kHalo + di;
             const int32_t gq = s_gb[kq];
             if (gq == -2) continue;
-            const int klo = me_low ? kme : kq, kup = me_low ? kq : kme;
-            float a = 0.0f;
-            for (int c = 0; c < C; ++c)
-                a += (s_G[klo * CM + c] + s_G[kup * CM + c]) * (s_I[kup * CM + c] - s_I[klo * CM + c]);
-            const float s = -0.5f * a;
+            const int klo = me_low ? kme : kq;
+            const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
             if (s == 0.0f) continue;
             const int iq = i + di, jq = j + dj;
             const int32_t rq = gq >= 0 ? (gq & kGbufIndexMask) : -1;
@@ -970,7 +1004,7 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             // exact edge values of this face at the neighbour: one step of 256 sub-pixels
             int64_t step[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) step[k] = (int64_t)(axis == 0 ? me.e.A[k] : me.e.B[k]) * (me_low ? 256 : -256);
+            for (int k = 0; k < 3; ++k) step[k] = (int64_t)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256 : -256);
             float omega;
             if (fq == f) {
                 omega = me_low ? 1.0f : 0.0f;
@@ -982,18 +1016,13 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
                 int64_t Eq[3];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) Eq[k] = Ep[k] + step[k];
-                bool mine_covers_other = inside(me.e, Eq);
+                bool mine_covers_other = inside(me, Eq);
                 if (!mine_covers_other && multi)
                     mine_covers_other = covers_face_multi(rp, frame_recs, fdata_frame, F, f, iq, jq);
                 const int sq = s_slot[kq];
                 EdgePart other;
-                if (sq >= 0) {
-                    RecRegs o;
-                    load_slot(T, sq, o);
-                    other = o.e;
-                } else {
-                    other = *reinterpret_cast<const EdgePart *>(&frame_recs[rq]);
-                }
+                if (sq >= 0) load_slot_edges(T, sq, other);
+                else other = *reinterpret_cast<const EdgePart *>(&frame_recs[rq]);
                 bool other_covers_me = edge_covers(other, i, j);
                 if (!other_covers_me && (gq & kGbufMulti))
                     other_covers_me = covers_face_multi(rq, frame_recs, fdata_frame, F, fq, i, j);
@@ -1002,12 +1031,12 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             }
             if (omega == 0.0f) continue;
             // midpoint: E(p) + E(q) = 2 E(p) + step
-            const float m0 = (2.0f * fEp[0] + (float)step[0]) * me.iw[0];
-            const float m1 = (2.0f * fEp[1] + (float)step[1]) * me.iw[1];
-            const float m2 = (2.0f * fEp[2] + (float)step[2]) * me.iw[2];
+            const float m0 = (2.0f * fEp[0] + (float)step[0]) * iw0;
+            const float m1 = (2.0f * fEp[1] + (float)step[1]) * iw1;
+            const float m2 = (2.0f * fEp[2] + (float)step[2]) * iw2;
             float lm[3];
             if (!fast_lambda(rr, multi, m0, m1, m2, lm)) continue;
-            const float Wm = (lm[0] * me.w[0] + lm[1] * me.w[1]) + lm[2] * me.w[2];
+            const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
             if (Wm == 0.0f) continue;
             const int ilo = me_low ? i : iq, jlo = me_low ? j : jq;
             const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
@@ -1030,15 +1059,12 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         return;
     }
 
-    // ---- phase C: segmented sum over runs of equal key along each 16-lane row (one DPP row),
-    // then the run tails add into the LDS slot accumulators (or global atomics without a slot)
+    // ---- phase C: segmented sum over runs of equal key along each 16-lane row (one DPP row); the
+    // run tails store their partial sums with plain LDS writes and push themselves onto their slot's
+    // list with one exchange (LDS float atomics serialise on shared addresses); tails without a
+    // slot (table full) add straight to global memory
     const int key = rp >= 0 ? rp : -1;
-    const int kl = dpp_shr_i<1>(key, -3);
-    int start = (lx == 0 || kl != key) ? lx : -1;
-    start = max(start, dpp_shr_i<1>(start, -1));
-    start = max(start, dpp_shr_i<2>(start, -1));
-    start = max(start, dpp_shr_i<4>(start, -1));
-    start = max(start, dpp_shr_i<8>(start, -1));
+    const int start = run_start(key, lx);
 #pragma unroll
     for (int v = 0; v < NVM; ++v) {
         if (AB & 32) break;
@@ -1051,14 +1077,15 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         acc[v] = x;
     }
     const int kr = dpp_shl_i<1>(key, -3);
-    const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key) && !(AB & 64);
+    const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key);
     float *gvb = grad_verts + (int64_t)b * V * 4;
     float *gcb = grad_colors + (int64_t)b * V * C;
     if (tail) {
         if (sp >= 0) {
 #pragma unroll
             for (int v = 0; v < NVM; ++v)
-                if (v < NV) atomicAdd(&s_vals[sp * NVM + v], acc[v]);
+                if (v < NV) s_part[t * NVM + v] = acc[v];
+            s_next[t] = atomicExch(&s_head[sp], t);
         } else {
             const FaceData &fd = fdata_frame[face_of_record(rp, F)];
             for (int v = 0; v < NV; ++v) {
@@ -1070,18 +1097,24 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     }
     __syncthreads();
 
-    // ---- phase D: flush, one wave-instruction of global atomics per (tile, record) with data
-    const int n = (AB & 8) ? 0 : nslots, wave = t >> 6, lane = t & 63;
-    if (lane < NV) {
-        const int k = lane < 9 ? lane / 3 : (lane - 9) / C;
-        const int comp = lane < 9 ? ((lane % 3) == 2 ? 3 : lane % 3) : (lane - 9) % C;
-        for (int e = wave; e < n; e += 4) {
-            const int slot = T.list[e];
-            const float val = s_vals[slot * NVM + lane];
-            if (val == 0.0f) continue;
-            const int vtx = T.v[k][slot];
-            if (lane < 9) atomicAdd(gvb + (int64_t)vtx * 4 + comp, val);
-            else atomicAdd(gcb + (int64_t)vtx * C + comp, val);
+    // ---- phase D: flush.  Thread t handles component t % NV of slot t / NV, so every lane of the
+    // workgroup walks one short list in parallel; a slot's components go out as one run of lanes
+    // (~3 cache lines of global float atomics per (tile, record)).
+    const int n = (AB & 8) ? 0 : nslots;
+    const int per_round = 256 / NV;
+    for (int e0 = 0; e0 < n; e0 += per_round) {
+        const int e = e0 + t / NV, comp_id = t - (t / NV) * NV;
+        if (t >= per_round * NV || e >= n) continue;
+        const int slot = T.list[e];
+        float val = 0.0f;
+        for (int q = s_head[slot]; q >= 0; q = s_next[q]) val += s_part[q * NVM + comp_id];
+        if (val == 0.0f) continue;
+        if (comp_id < 9) {
+            const int k = comp_id / 3, c3 = comp_id % 3;
+            atomicAdd(gvb + (int64_t)T.v[k][slot] * 4 + (c3 == 2 ? 3 : c3), val);
+        } else {
+            const int k = (comp_id - 9) / C, c = (comp_id - 9) % C;
+            atomicAdd(gcb + (int64_t)T.v[k][slot] * C + c, val);
         }
     }
 }
