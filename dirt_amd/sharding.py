@@ -1,0 +1,56 @@
+"""Frame-sharded batched rasterisation across the GPUs of one node (one process per GPU).
+
+The reference has no multi-GPU data path: tests/multi_gpu_test.py:20-29 places two independent renders
+on /gpu:0 and /gpu:1 of one session, and GlDispatcher keeps one GL thread per CUDA context
+(csrc/gl_dispatcher.h:101-108).  Frames of a batch are independent in both forward and backward
+(SURVEY 8e), so the MI355X design shards the batch dimension contiguously over ranks and runs each
+shard with no collective in the data path.  The only optional exchange is gathering the rendered
+frames (RCCL all-gather over xGMI with the "nccl" backend; gloo works for CPU tensors in tests).
+"""
+import torch
+import torch.distributed as dist
+
+from .rasterise_ops import rasterise_batch
+
+
+def shard_bounds(batch, rank, world):
+    """Contiguous [lo, hi) frame range of `rank`; the first batch % world ranks take one extra frame."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad rank/world: %r/%r" % (rank, world))
+    base, extra = divmod(int(batch), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def gather_frames(local, batch, group=None):
+    """All-gather per-rank frame blocks [b_r, ...] into the full batch [batch, ...] on every rank.
+
+    Pads every block to the largest shard so one all_gather (RCCL ring over xGMI) moves it."""
+    world = dist.get_world_size(group)
+    sizes = [shard_bounds(batch, r, world) for r in range(world)]
+    mx = max(hi - lo for lo, hi in sizes)
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
+
+
+def rasterise_batch_sharded(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
+                            channels=None, group=None, gather=False, render=rasterise_batch):
+    """rasterise_batch over this rank's contiguous share of the frames.
+
+    Every rank passes the full batch (or any object supporting slicing on dim 0); the rank renders
+    frames [lo, hi) and returns (pixels_local, (lo, hi)), or the gathered full batch if `gather`.
+    Gradients flow through pixels_local like rasterise_batch; the gathered tensor is forward-only.
+    `render` is the per-shard renderer (the HIP op by default)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    B = background.shape[0]
+    lo, hi = shard_bounds(B, rank, world)
+    local = render(background[lo:hi], vertices[lo:hi], vertex_colors[lo:hi], faces[lo:hi], camera_pos=camera_pos,
+                   height=height, width=width, channels=channels)
+    if not gather or world == 1:
+        return local, (lo, hi)
+    with torch.no_grad():
+        return gather_frames(local.detach(), B, group=group)

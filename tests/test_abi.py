@@ -1,0 +1,77 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports every symbol include/dirt_mi355x.h declares,
+and validates arguments (reference OP_REQUIRES messages, csrc/rasterise_egl.cpp:310-336) before touching
+the GPU.  No compute call is made here (there is no GPU in this container)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from dirt_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dirt_mi355x.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dirt_\w+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("dirt_rasterise_fwd", "dirt_rasterise_bwd", "dirt_workspace_sizes", "dirt_last_error"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the Python binding knows the signature of each
+    assert set(declared_functions()) <= set(_lib.SIGNATURES)
+
+
+def test_abi_version_and_workspace_sizes():
+    lib = _lib.load()
+    assert lib.dirt_abi_version() == 2
+    saved, scratch = _lib.workspace_sizes(1, 1024, 1024, 3, 150000, 50000)
+    assert saved >= 50000 * 6 * 128 + 50000 * 32  # 128-B records (6 slots/face) + 32-B face data
+    assert scratch > 0
+    s2, _ = _lib.workspace_sizes(2, 1024, 1024, 3, 150000, 50000)
+    assert s2 >= 2 * saved - 512
+
+
+@pytest.mark.parametrize("args,msg", [
+    ((1, 128, 128, 9, 4, 2), "channels"),
+    ((1, 128, 128, 0, 4, 2), "channels"),
+    ((1, 0, 128, 3, 4, 2), "height, width"),
+    ((1, 128, 9000, 3, 4, 2), "height, width"),
+    ((-1, 128, 128, 3, 4, 2), "non-negative"),
+    ((1, 128, 128, 3, 4, (1 << 26) + 1), "too large"),
+])
+def test_invalid_arguments_raise_before_any_gpu_call(args, msg):
+    with pytest.raises(ValueError, match=msg):
+        _lib.workspace_sizes(*args)
+    lib = _lib.load()
+    B, H, W, C, V, F = args
+    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, B, H, W, C, V, F, 0, None, None, None, 0, None, 0, 0, None)
+    assert rc == _lib.DIRT_EINVAL
+    assert msg in lib.dirt_last_error().decode()
+
+
+def test_null_pointers_and_bad_shader_rejected():
+    lib = _lib.load()
+    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, 1, 16, 16, 3, 3, 1, 0, None, None, None, 0, None, 0, 0, None)
+    assert rc == _lib.DIRT_EINVAL and "null" in lib.dirt_last_error().decode()
+    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, 1, 16, 16, 3, 3, 1, 77, None, None, None, 0, None, 0, 0, None)
+    assert rc == _lib.DIRT_EINVAL and "shader" in lib.dirt_last_error().decode()
+    rc = lib.dirt_rasterise_bwd(None, None, None, None, None, None, None, 1, 16, 16, 3, 3, 1, None, None, None, None)
+    assert rc == _lib.DIRT_EINVAL
+
+
+def test_zero_batch_is_a_no_op():
+    lib = _lib.load()
+    assert lib.dirt_rasterise_fwd(None, None, None, None, None, 0, 16, 16, 3, 3, 1, 0, None, None, None, 0, None, 0, 0,
+                                  None) == _lib.DIRT_OK

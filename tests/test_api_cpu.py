@@ -1,0 +1,87 @@
+"""CPU tests of the Python op surface (mirror of the reference dirt/rasterise_ops.py) and helpers."""
+import inspect
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import dirt_amd
+from dirt_amd import lighting, matrices, rasterise_ops
+
+
+def test_op_names_and_signatures_match_the_reference():
+    # dirt/rasterise_ops.py:10,57,91,110,129,148,167,186 (camera_pos made optional)
+    for name in ("rasterise", "rasterise_batch"):
+        params = list(inspect.signature(getattr(dirt_amd, name)).parameters)
+        assert params == ["background", "vertices", "vertex_colors", "faces", "camera_pos", "height", "width",
+                          "channels", "name"]
+        sig = inspect.signature(getattr(dirt_amd, name))
+        assert all(sig.parameters[p].default is None for p in params[4:])
+    for name in ("rasterise_grad", "oceanic_no_cloud", "oceanic_simple_proxy", "oceanic_still_cloud",
+                 "oceanic_opt_flow", "hill"):
+        assert callable(getattr(dirt_amd, name))
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_no_cpu_fallback():
+    bg = np.zeros((8, 8, 3), np.float32)
+    with pytest.raises(RuntimeError, match="GPU"):
+        dirt_amd.rasterise(bg, np.zeros((3, 4), np.float32), np.zeros((3, 3), np.float32), [[0, 1, 2]])
+
+
+@pytest.mark.parametrize("shapes,msg", [
+    (((1, 8, 8, 3), (1, 3, 4), (1, 3, 3), (1, 1, 3)), None),
+    (((1, 8, 9, 3), (1, 3, 4), (1, 3, 3), (1, 1, 3)), "background"),
+    (((1, 8, 8, 3), (1, 3, 3), (1, 3, 3), (1, 1, 3)), "vertices"),
+    (((1, 8, 8, 3), (1, 3, 4), (1, 4, 3), (1, 1, 3)), "vertex_colors"),
+    (((1, 8, 8, 3), (1, 3, 4), (1, 3, 3), (1, 1, 2)), "faces"),
+    (((2, 8, 8, 3), (1, 3, 4), (1, 3, 3), (1, 1, 3)), "batch"),
+])
+def test_shape_validation_messages(shapes, msg):
+    ts = [torch.zeros(s) for s in shapes]
+    if msg is None:
+        rasterise_ops._check_shapes(*ts, 8, 8, 3)
+    else:
+        with pytest.raises(ValueError, match=msg):
+            rasterise_ops._check_shapes(*ts, 8, 8, 3)
+
+
+def test_procedural_ops_not_yet_available():
+    with pytest.raises(NotImplementedError):
+        dirt_amd.hill(None, None, None, None, None)
+
+
+def test_matrices_match_reference_formulas():
+    P = matrices.perspective_projection(0.1, 20.0, 0.2, 0.75).numpy()
+    n, f, r, t = 0.1, 20.0, 0.2, 0.2 * 0.75
+    expect = np.array([[n / r, 0, 0, 0], [0, n / t, 0, 0], [0, 0, -(f + n) / (f - n), -2 * f * n / (f - n)],
+                       [0, 0, -1, 0]], np.float32).T
+    np.testing.assert_allclose(P, expect, rtol=1e-6)
+    R = matrices.rodrigues([0.0, 0.5, 0.0]).numpy()
+    np.testing.assert_allclose(R[:3, :3] @ R[:3, :3].T, np.eye(3), atol=1e-6)
+    c, s = math.cos(0.5), math.sin(0.5)
+    # K = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]] indexed (in, out): dirt/matrices.py:41-45
+    np.testing.assert_allclose(R[:3, :3], [[c, 0, s], [0, 1, 0], [-s, 0, c]], atol=1e-6)
+    T = matrices.translation([1.0, 2.0, 3.0]).numpy()
+    np.testing.assert_allclose(np.array([0, 0, 0, 1.0]) @ T, [1, 2, 3, 1])
+    np.testing.assert_allclose(matrices.compose(T, R).numpy(), T @ R, atol=1e-6)
+    assert torch.equal(matrices.compose(), torch.eye(4))
+
+
+def test_lighting_helpers():
+    verts = torch.tensor([[0., 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]])
+    faces = torch.tensor([[0, 1, 2], [0, 1, 3]])
+    sv, sf = lighting.split_vertices_by_face(verts, faces)
+    assert sv.shape == (6, 3) and sf.tolist() == [[0, 1, 2], [3, 4, 5]]
+    n = lighting.vertex_normals_pre_split(sv, sf)
+    np.testing.assert_allclose(n[:3].numpy(), [[0, 0, 1]] * 3, atol=1e-6)
+    np.testing.assert_allclose(n[3:].numpy(), [[0, -1, 0]] * 3, atol=1e-6)
+    vn = lighting.vertex_normals(verts, faces)
+    np.testing.assert_allclose(torch.linalg.norm(vn[:2], dim=-1).numpy(), 1.0, atol=1e-6)
+    d = lighting.diffuse_directional(n, torch.ones(6, 3), [0., 0., -1.], [1., 0.5, 0.25])
+    np.testing.assert_allclose(d[0].numpy(), [1, 0.5, 0.25], atol=1e-6)
+    p = lighting.diffuse_point(sv, n, torch.ones(6, 3), [0., 0., 5.], [1., 1., 1.])
+    assert p.shape == (6, 3) and float(p.min()) >= 0
+    sp = lighting.specular_directional(sv, n, torch.ones(6, 3), [0., 0., -1.], [1., 1., 1.], [0., 0., 3.], 6.0)
+    assert sp.shape == (6, 3)

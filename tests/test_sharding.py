@@ -1,0 +1,82 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the frame-sharded batch path (dirt_amd.sharding).
+
+The HIP renderer needs a GPU, so the per-shard renderer here is the CPU oracle; what is under test is
+the partition, the no-collective local path and the all-gather of the rendered frames
+(reference multi-device check: tests/multi_gpu_test.py:6-29, SURVEY 8c 'Multi-device').
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import scenes
+from dirt_amd.sharding import gather_frames, rasterise_batch_sharded, shard_bounds
+from oracle import oracle
+
+
+def test_shard_bounds_partition():
+    for B in (0, 1, 5, 8, 64, 65):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(B, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == B
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_bounds(4, 2, 2)
+
+
+def _oracle_render(bg, v, c, f, camera_pos=None, height=None, width=None, channels=None):
+    px, _, _ = oracle.rasterise_fwd(bg.numpy(), v.numpy(), c.numpy(), f.numpy())
+    return torch.from_numpy(px)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, inputs, outq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bg, v, c, f = (torch.from_numpy(a) for a in inputs)
+        local, (lo, hi) = rasterise_batch_sharded(bg, v, c, f, render=_oracle_render)
+        full = gather_frames(local, bg.shape[0])
+        full2 = rasterise_batch_sharded(bg, v, c, f, render=_oracle_render, gather=True)
+        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [5, 4])
+def test_two_rank_sharded_batch_matches_single_process(B):
+    inputs = scenes.batch_of(scenes.random_triangles, B, F=150, W=40, H=32, radius_px=8.0, seed=3)
+    ref, _, _ = oracle.rasterise_fwd(*inputs)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, inputs, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    covered = []
+    for rank, lo, hi, local, full, full2 in res:
+        assert (lo, hi) == shard_bounds(B, rank, 2)
+        np.testing.assert_array_equal(local, ref[lo:hi])   # each rank renders only its frames
+        np.testing.assert_array_equal(full, ref)           # all-gather reassembles the batch
+        np.testing.assert_array_equal(full2, ref)
+        covered.extend(range(lo, hi))
+    assert covered == list(range(B))
