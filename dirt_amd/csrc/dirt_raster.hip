@@ -26,6 +26,7 @@
 #include <string>
 #include <utility>
 #include <vector>
+#include <algorithm>
 
 #include "../../include/dirt_mi355x.h"
 #include "raster_rules.h"
@@ -298,10 +299,12 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
             }
         } else {
             frame_recs[f] = r;  // empty unless clip_face overwrites it
+#ifndef DIRT_SETUP_NO_CLIP
             if (ok) {
                 nsub = clip_face(tri, W, H, F, f, frame_recs);
                 fd.clipped = 1;
             }
+#endif
             for (int s = 0; s < nsub; ++s) {
                 uint32_t bx, by;
                 load_bbox(frame_recs[rec_index(F, f, s)], bx, by);
@@ -469,7 +472,8 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
 
 constexpr int kStrips = 4;
 constexpr int kSmallEdge = 1 << 16;
-constexpr int kListCap = 512;      // per-wave survivor list (filtered record indices)
+constexpr int kListCap = 256;      // per-wave survivor list (filtered record indices)
+constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per round (2 loads per lane in flight)
 constexpr int32_t kLargeFlag = (int32_t)0x80000000;
 
 struct alignas(16) StripEntry {  // 64 B of wave-private LDS per staged triangle
@@ -549,7 +553,9 @@ __device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_
     return __popcll(mask);
 }
 
-template <int CC>
+// AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
+// staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
+template <int CC, int AB = 0>
 __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ ccount,
@@ -595,22 +601,25 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const uint32_t rx0 = (uint32_t)(si0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
     const uint32_t ry0 = (uint32_t)(sj0 - (cy << cshift)), ry1 = ry0 + 3;
 
-    if (off + cnt <= (uint64_t)capacity) {
+    if (AB & 8) {
+        st.best_rec = (int32_t)(cnt + off);
+    } else if (off + cnt <= (uint64_t)capacity) {
         int n_s = 0;
-        for (uint32_t blk = 0;; blk += 256) {
+        for (uint32_t blk = 0;; blk += kFilterBlock) {
             const bool more = blk < cnt;
             if (more) {
-                // a. filter the coarse bin (4 independent loads per lane in flight)
-                uint2 ev[4];
-                bool ok[4];
+                // a. filter the coarse bin (independent loads per lane in flight)
+                constexpr int U = kFilterBlock / 64;
+                uint2 ev[U];
+                bool ok[U];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < U; ++u) {
                     const uint32_t idx = blk + u * 64 + lane;
                     ok[u] = idx < cnt;
                     ev[u] = ok[u] ? bins[off + idx] : make_uint2(0u, 0u);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < U; ++u) {
                     const uint32_t bb = ev[u].y;
                     const bool keep = ok[u] && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 &&
                                       ((bb >> 16) & 0xff) <= ry1 && (bb >> 24) >= ry0;
@@ -624,15 +633,27 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                 }
             }
             if (n_s == 0 && !more) break;
-            if (n_s < kListCap - 256 && more) continue;
+            if (n_s < kListCap - kFilterBlock && more) continue;
             wave_lds_sync();
+            if (AB & 2) {
+                st.best_rec += s_list[lane & (kListCap - 1)] + n_s;
+                n_s = 0;
+                if (!more) break;
+                continue;
+            }
             // b + c: stage and rasterise the collected survivors, 64 at a time
             for (int from = 0; from < n_s; from += 64) {
                 const int m = min(64, n_s - from);
                 const int ne = stage_strip(frame_recs, s_list, from, m, si0, sj0, s_ent, lane);
                 wave_lds_sync();
+                if (AB & 1) {
+                    if (ne > 0) st.best_rec += s_ent[lane % ne].face;
+                    wave_lds_sync();
+                    continue;
+                }
+#pragma unroll 2
                 for (int e = 0; e < ne; ++e) {
-                    const StripEntry &R = s_ent[e];
+                    const StripEntry R = s_ent[e];  // one 64-B broadcast read
                     const int32_t rif = __builtin_amdgcn_readfirstlane(R.ri);
                     bool in;
                     if (rif >= 0) {
@@ -646,7 +667,14 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                         edge_values(r, i, j, E);
                         in = inside(r, E);
                     }
-                    if (in) depth_update(R.za, R.zb, R.fx0, R.fy0, R.z0, R.face, rif & 0x7fffffff, fxl, fyl, st);
+                    // R4 without branches (same operation order as sample_depth)
+                    const float zw = (R.za * (fxl - R.fx0) + R.zb * (fyl - R.fy0)) + R.z0;
+                    const uint32_t q = (uint32_t)(__builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f) * 16777215.0f + 0.5f);
+                    const bool ok = in && zw >= 0.0f && zw <= 1.0f && q < kDepthMax;
+                    const uint64_t key = ((uint64_t)q << 32) | (uint32_t)R.face;
+                    const bool win = ok && key < st.best;
+                    st.best = win ? key : st.best;
+                    st.best_rec = win ? (rif & 0x7fffffff) : st.best_rec;
                 }
                 wave_lds_sync();
             }
@@ -671,6 +699,10 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 
     if (!in_frame) return;
     float *out = pixels + o * C;
+    if (AB & 7) {
+        gbuffer[o] = st.best_rec;
+        return;
+    }
     if (st.best_rec < 0) {
         gbuffer[o] = -1;
 #pragma unroll
@@ -1119,6 +1151,24 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     }
 }
 
+// zero two float arrays in one launch (the backward's atomically accumulated outputs)
+__global__ __launch_bounds__(256) void zero2_kernel(float *__restrict__ a, int64_t na, float *__restrict__ b, int64_t nb)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // a is 16-B aligned (torch / caller allocations); vector part then tail
+    const int64_t na4 = na / 4, nb4 = nb / 4;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t k = gid; k < na4; k += stride) reinterpret_cast<float4 *>(a)[k] = z;
+    for (int64_t k = na4 * 4 + gid; k < na; k += stride) a[k] = 0.0f;
+    if ((reinterpret_cast<uintptr_t>(b) & 15) == 0) {
+        for (int64_t k = gid; k < nb4; k += stride) reinterpret_cast<float4 *>(b)[k] = z;
+        for (int64_t k = nb4 * 4 + gid; k < nb; k += stride) b[k] = 0.0f;
+    } else {
+        for (int64_t k = gid; k < nb; k += stride) b[k] = 0.0f;
+    }
+}
+
 __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n, int V, uint32_t *flag)
 {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
@@ -1236,8 +1286,10 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
     if (V > 0) {
-        HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)B * V * 4 * sizeof(float), stream));
-        HIP_TRY(hipMemsetAsync(grad_vertex_colors, 0, (size_t)B * V * C * sizeof(float), stream));
+        const int64_t na = (int64_t)B * V * 4, nb = (int64_t)B * V * C;
+        const int64_t blocks = std::min<int64_t>(2048, (na / 4 + 255) / 256 + 1);
+        zero2_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(grad_vertices, na, grad_vertex_colors, nb);
+        HIP_TRY(hipGetLastError());
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_GRAD, stream);
@@ -1250,6 +1302,49 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     else LAUNCH_GRAD(0);
 #undef LAUNCH_GRAD
     HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+// Ablation entry point (tools/ablate.py): re-runs raster_kernel (C == 3) on the bins a preceding
+// dirt_rasterise_fwd left in `scratch`, with parts switched off; returns the kernel time in ms.
+int dirt_debug_raster_variant(int variant, const float *background, const float *vertex_colors, int B, int H, int W,
+                              int C, int V, int F, float *pixels, int32_t *gbuffer, const void *saved,
+                              const void *scratch, void *stream_, float *ms)
+{
+    if (C != 3) return fail(DIRT_EINVAL, "dirt_debug_raster_variant: C must be 3");
+    Layout L;
+    int rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const char *sv = static_cast<const char *>(saved), *sc = static_cast<const char *>(scratch);
+    const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
+    const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    const uint32_t *ccount = reinterpret_cast<const uint32_t *>(sc + L.off_count);
+    const uint64_t *coffset = reinterpret_cast<const uint64_t *>(sc + L.off_offset);
+    const uint2 *bins = reinterpret_cast<const uint2 *>(sc + L.off_bins);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, stream));
+    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+#define V_RAST(AB)                                                                                                 \
+    case AB:                                                                                                       \
+        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, coffset, \
+                                                             bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift, \
+                                                             L.nctx, L.ncoarse, L.nrec, pixels, gbuffer);          \
+        break
+    switch (variant) {
+        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8);
+    default:
+        return fail(DIRT_EINVAL, "dirt_debug_raster_variant: unknown variant");
+    }
+#undef V_RAST
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    HIP_TRY(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return DIRT_OK;
 }
 

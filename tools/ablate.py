@@ -42,7 +42,21 @@ def main():
             if rnd >= 3:
                 res[k].append(ms.value * 1e3)
     for k, name in NAMES.items():
-        print("%-22s median %8.2f us  min %8.2f" % (name, np.median(res[k]), np.min(res[k])))
+        print("grad   %-28s median %8.2f us  min %8.2f" % (name, np.median(res[k]), np.min(res[k])))
+    rfn = lib.dirt_debug_raster_variant
+    rfn.argtypes = [ctypes.c_int, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, P, ctypes.POINTER(ctypes.c_float)]
+    rfn.restype = ctypes.c_int
+    RN = {0: "full", 1: "no pixel loop", 2: "bin filter only", 4: "no resolve", 8: "nothing (io only)"}
+    rres = {k: [] for k in RN}
+    for rnd in range(30):
+        for k in RN:
+            _lib.check(rfn(k, t[0].data_ptr(), t[2].data_ptr(), B, H, W, C, V, F, sess.pixels.data_ptr(),
+                           sess.gbuffer.data_ptr(), sess.saved.data_ptr(), sess.scratch.data_ptr(), stream,
+                           ctypes.byref(ms)))
+            if rnd >= 3:
+                rres[k].append(ms.value * 1e3)
+    for k, name in RN.items():
+        print("raster %-28s median %8.2f us  min %8.2f" % (name, np.median(rres[k]), np.min(rres[k])))
 
 
 if __name__ == "__main__":
