@@ -24,6 +24,10 @@ $(LIB): $(HIP_DEPS)
 $(ORACLE): oracle/dirt_oracle.c
 	$(CC) $(ORACLE_CFLAGS) -shared -o $@ $< -lm
 
+# experiment builds: make variant NAME=w5 DEFS=-DDIRT_GRAD_WAVES=5  -> build/variants/w5.so
+variant: $(HIP_DEPS)
+	mkdir -p build/variants && $(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o build/variants/$(NAME).so $(HIP_SRC)
+
 asm: $(HIP_DEPS)
 	mkdir -p build/asm && cd build/asm && $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o dirt_raster.s ../../$(HIP_SRC)
 

@@ -651,7 +651,6 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                     wave_lds_sync();
                     continue;
                 }
-#pragma unroll 2
                 for (int e = 0; e < ne; ++e) {
                     const StripEntry R = s_ent[e];  // one 64-B broadcast read
                     const int32_t rif = __builtin_amdgcn_readfirstlane(R.ri);
@@ -805,6 +804,10 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
     return true;
 }
 
+#ifndef DIRT_GRAD_WAVES
+#define DIRT_GRAD_WAVES 4  // min waves per SIMD the register allocation must allow
+#endif
+
 constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
 constexpr int kHaloPix = kHalo * kHalo;
 constexpr int kSlots = 128;        // distinct records per tile+halo kept in LDS (typ. 10-40)
@@ -864,7 +867,7 @@ __device__ __forceinline__ int run_start(int key, int lx)
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
 // 32 skip the DPP run scan (every lane adds into LDS)
 template <int CC, int AB = 0>
-__global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+__global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
                                                    int V, int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
@@ -879,12 +882,18 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     __shared__ int32_t s_slot[kHaloPix];
     __shared__ float s_sx[kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), see DESIGN.md 4
     __shared__ float s_sy[kHaloPix];
-    __shared__ __attribute__((aligned(16))) float s_G[kHaloPix * CP];
-    __shared__ __attribute__((aligned(16))) float s_I[kHaloPix * CP];
+    // G / I of the staged pixels (phases A-B), then reused for the run-tail partial sums (C-D):
+    // keeps the workgroup at ~26 KB of LDS (6 per CU)
+    constexpr int kUnion = 2 * kHaloPix * CP;
+    constexpr int kTailCap = kUnion / NVM;
+    __shared__ __attribute__((aligned(16))) float s_u[kUnion];
+    float *const s_G = s_u;
+    float *const s_I = s_u + kHaloPix * CP;
+    float *const s_part = s_u;
     __shared__ SlotTable T;
-    __shared__ float s_part[256 * NVM];  // run-tail partial sums, indexed by thread id
     __shared__ int32_t s_head[kSlots];   // per slot: linked list of its run tails
-    __shared__ int32_t s_next[256];
+    __shared__ int32_t s_next[kTailCap];
+    __shared__ int32_t s_ntail;
 
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
@@ -901,7 +910,10 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         T.key[k] = -1;
         s_head[k] = -1;
     }
-    if (t == 0) T.n = 0;
+    if (t == 0) {
+        T.n = 0;
+        s_ntail = 0;
+    }
     const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
     for (int k = t; k < kHaloPix; k += 256) {
         const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
@@ -1008,16 +1020,11 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
         float fEp[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) fEp[k] = fast_i64_to_f32(Ep[k]);
-        float lam[3];
-        if (!(AB & 2) && fast_lambda(rr, multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
-            float Gm[CM];
-#pragma unroll
-            for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * Gm[c];
-        }
-        // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window)
+        // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window).
+        // Pass 1 decides ownership (exact integer coverage tests) into 2-bit codes (0 skip, 1 half,
+        // 2 whole); pass 2 interpolates and accumulates.  Splitting keeps the coverage tests' and the
+        // accumulators' registers apart (occupancy).
+        uint32_t codes = 0;
 #pragma unroll
         for (int dir = 0; dir < 4; ++dir) {
             if (AB & 1) break;
@@ -1030,27 +1037,23 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
             const int klo = me_low ? kme : kq;
             const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
             if (s == 0.0f) continue;
-            const int iq = i + di, jq = j + dj;
             const int32_t rq = gq >= 0 ? (gq & kGbufIndexMask) : -1;
             const int fq = rq >= 0 ? face_of_record(rq, F) : -1;
-            // exact edge values of this face at the neighbour: one step of 256 sub-pixels
-            int64_t step[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) step[k] = (int64_t)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256 : -256);
-            float omega;
+            uint32_t code;
             if (fq == f) {
-                omega = me_low ? 1.0f : 0.0f;
+                code = me_low ? 2u : 0u;
             } else if (fq < 0) {
-                omega = 1.0f;
+                code = 2u;
             } else if (AB & 16) {
-                omega = 0.5f;
+                code = 1u;
             } else {
                 int64_t Eq[3];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) Eq[k] = Ep[k] + step[k];
+                for (int k = 0; k < 3; ++k)
+                    Eq[k] = Ep[k] + (int64_t)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256 : -256);
                 bool mine_covers_other = inside(me, Eq);
                 if (!mine_covers_other && multi)
-                    mine_covers_other = covers_face_multi(rp, frame_recs, fdata_frame, F, f, iq, jq);
+                    mine_covers_other = covers_face_multi(rp, frame_recs, fdata_frame, F, f, i + di, j + dj);
                 const int sq = s_slot[kq];
                 EdgePart other;
                 if (sq >= 0) load_slot_edges(T, sq, other);
@@ -1058,19 +1061,32 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
                 bool other_covers_me = edge_covers(other, i, j);
                 if (!other_covers_me && (gq & kGbufMulti))
                     other_covers_me = covers_face_multi(rq, frame_recs, fdata_frame, F, fq, i, j);
-                omega = (!mine_covers_other && other_covers_me) ? 1.0f
-                        : (mine_covers_other && !other_covers_me) ? 0.0f : 0.5f;
+                code = (!mine_covers_other && other_covers_me) ? 2u : (mine_covers_other && !other_covers_me) ? 0u : 1u;
             }
-            if (omega == 0.0f) continue;
-            // midpoint: E(p) + E(q) = 2 E(p) + step
-            const float m0 = (2.0f * fEp[0] + (float)step[0]) * iw0;
-            const float m1 = (2.0f * fEp[1] + (float)step[1]) * iw1;
-            const float m2 = (2.0f * fEp[2] + (float)step[2]) * iw2;
+            codes |= code << (2 * dir);
+        }
+#pragma unroll
+        for (int dir = 0; dir < 4; ++dir) {
+            const uint32_t code = (codes >> (2 * dir)) & 3u;
+            if (code == 0u) continue;
+            const int axis = dir >> 1;
+            const bool me_low = (dir & 1) == 0;
+            const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
+            const int klo = me_low ? kme : kme + dj * kHalo + di;
+            const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
+            const float omega = code == 2u ? 1.0f : 0.5f;
+            // midpoint: E(p) + E(q) = 2 E(p) + step, step = one pixel (256 sub-pixels) of the edge
+            float m[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float st = (float)((int64_t)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256 : -256));
+                m[k] = (2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2);
+            }
             float lm[3];
-            if (!fast_lambda(rr, multi, m0, m1, m2, lm)) continue;
+            if (!fast_lambda(rr, multi, m[0], m[1], m[2], lm)) continue;
             const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
             if (Wm == 0.0f) continue;
-            const int ilo = me_low ? i : iq, jlo = me_low ? j : jq;
+            const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
             const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
             const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
             const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
@@ -1081,6 +1097,23 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
                 acc[k * 3 + axis] += g;
                 acc[k * 3 + 2] -= g * ndc;
             }
+        }
+    }
+    if (rp >= 0) {
+        // colour weights last: keeps their registers out of the pair loop's live range
+        const Rec &rr = frame_recs[rp];
+        const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+        int64_t Ep[3];
+        edge_values(me, i, j, Ep);
+        float lam[3];
+        if (!(AB & 2) && fast_lambda(rr, (gp & kGbufMulti) != 0, fast_i64_to_f32(Ep[0]) * rr.iw[0],
+                                     fast_i64_to_f32(Ep[1]) * rr.iw[1], fast_i64_to_f32(Ep[2]) * rr.iw[2], lam)) {
+            float Gm[CM];
+#pragma unroll
+            for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * Gm[c];
         }
     }
     if (AB & 4) {
@@ -1112,12 +1145,25 @@ __global__ __launch_bounds__(256) void grad_kernel(const float *__restrict__ pix
     const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key);
     float *gvb = grad_verts + (int64_t)b * V * 4;
     float *gcb = grad_colors + (int64_t)b * V * C;
+    __syncthreads();  // every read of s_G / s_I is done: the union now holds tail partials
+    int q = -1;
+    {
+        const bool want = tail && sp >= 0;
+        const uint64_t mask = __ballot(want);
+        int base = 0;
+        if ((t & 63) == 0 && mask) base = atomicAdd(&s_ntail, __popcll(mask));
+        base = __shfl(base, 0, 64);
+        if (want) {
+            q = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            if (q >= kTailCap) q = -1;
+        }
+    }
     if (tail) {
-        if (sp >= 0) {
+        if (q >= 0) {
 #pragma unroll
             for (int v = 0; v < NVM; ++v)
-                if (v < NV) s_part[t * NVM + v] = acc[v];
-            s_next[t] = atomicExch(&s_head[sp], t);
+                if (v < NV) s_part[q * NVM + v] = acc[v];
+            s_next[q] = atomicExch(&s_head[sp], q);
         } else {
             const FaceData &fd = fdata_frame[face_of_record(rp, F)];
             for (int v = 0; v < NV; ++v) {
