@@ -553,6 +553,24 @@ __device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_
     return __popcll(mask);
 }
 
+// per-workgroup phase timestamps of the instrumented backward (AB & 128, dirt_debug_bwd_variant 128)
+constexpr int kTsMaxWG = 1 << 16;
+constexpr int kTsStride = 13;  // 8 phase timestamps, HW_ID, XCC_ID, 3 inside phase B (wave 0)
+__device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
+#define PHASE_TS(n)                                                                                           \
+    do {                                                                                                      \
+        if ((AB & 128) && threadIdx.x == 0) {                                                                 \
+            const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                              \
+            if (wg_ < kTsMaxWG) {                                                                             \
+                g_phase_ts[wg_ * kTsStride + (n)] = __builtin_amdgcn_s_memtime();                             \
+                if ((n) == 0) {                                                                               \
+                    g_phase_ts[wg_ * kTsStride + 8] = __builtin_amdgcn_s_getreg((4) | (31 << 11));            \
+                    g_phase_ts[wg_ * kTsStride + 9] = __builtin_amdgcn_s_getreg((20) | (31 << 11));           \
+                }                                                                                             \
+            }                                                                                                 \
+        }                                                                                                     \
+    } while (0)
+
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
 template <int CC, int AB = 0>
@@ -767,7 +785,7 @@ __device__ __forceinline__ bool covers_face(const EdgePart &hint, int64_t hint_r
 template <int D>
 __device__ __forceinline__ float dpp_shr_f(float v)  // lane l <- lane l-D of the same 16-lane row, 0 if none
 {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x110 + D, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x110 + D, 0xF, 0xF, true));
 }
 template <int D>
 __device__ __forceinline__ int dpp_shr_i(int v, int fill)
@@ -822,6 +840,7 @@ struct SlotTable {
     int64_t C[3][kSlots];
     uint32_t bx[kSlots], by[kSlots];
     int32_t v[3][kSlots];
+    float iw[3][kSlots], w[3][kSlots];  // interpolation data of the record (own-pixel path)
     int32_t n;
 };
 
@@ -901,11 +920,14 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
     const int i = tx * kTile + lx, j = ty * kTile + ly;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
-    const float inv_hw = 2.0f / (float)W, inv_hh = 2.0f / (float)H;
+    // uniform: readfirstlane (convergent) keeps the divisions at the top instead of in every pair branch
+    const float inv_hw = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 2.0f / (float)W)));
+    const float inv_hh = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 2.0f / (float)H)));
     const int kme = (ly + 1) * kHalo + (lx + 1);
     const bool in_frame = i < W && j < H;
 
     // ---- phase A: stage g-buffer / G / I of the tile + one-pixel halo, pair scalars, slot table
+    PHASE_TS(0);
     for (int k = t; k < kSlots; k += 256) {
         T.key[k] = -1;
         s_head[k] = -1;
@@ -935,6 +957,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         }
     }
     __syncthreads();
+    PHASE_TS(1);
     const int32_t gp = in_frame ? s_gb[kme] : -2;
     {
         // pair scalars for pairs starting at a staged pixel (same operand order as the oracle)
@@ -967,15 +990,16 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         if (key >= 0 && start == lx) slot = slot_insert(T, key);
         slot = __shfl(slot, (t & 48) + start, 64);
         s_slot[kme] = key >= 0 ? slot : -1;
+        for (int k = t; k < kHaloPix; k += 256) {
+            const int hx = k % kHalo, hy = k / kHalo;
+            if (hx != 0 && hy != 0 && hx != kHalo - 1 && hy != kHalo - 1) continue;
+            const int32_t g = s_gb[k];
+            s_slot[k] = g >= 0 ? slot_insert(T, g) : -1;
+        }
     }
     __syncthreads();
-    for (int k = t; k < kHaloPix; k += 256) {
-        const int hx = k % kHalo, hy = k / kHalo;
-        if (hx != 0 && hy != 0 && hx != kHalo - 1 && hy != kHalo - 1) continue;
-        const int32_t g = s_gb[k];
-        s_slot[k] = g >= 0 ? slot_insert(T, g) : -1;
-    }
-    __syncthreads();
+    PHASE_TS(2);
+    PHASE_TS(3);
     const int nslots = T.n;
     for (int e = t; e < nslots; e += 256) {
         const int s = T.list[e];
@@ -989,8 +1013,15 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         }
         T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16);
         T.by[s] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
+        const Rec &r = frame_recs[ri];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            T.iw[k][s] = r.iw[k];
+            T.w[k][s] = fd.w[k];
+        }
     }
     __syncthreads();
+    PHASE_TS(4);
 
     // ---- phase B: per-pixel contributions to the face visible at this pixel
     const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
@@ -1010,11 +1041,19 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         // vector-memory path (L1-resident: a wave touches a handful of records).
         const int f = face_of_record(rp, F);
         const bool multi = (gp & kGbufMulti) != 0;
-        const Rec &rr = frame_recs[rp];
-        const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
-        const float iw0 = rr.iw[0], iw1 = rr.iw[1], iw2 = rr.iw[2];
-        const FaceData &fdr = fdata_frame[f];
-        const float w0 = fdr.w[0], w1 = fdr.w[1], w2 = fdr.w[2];
+        const Rec &rr = frame_recs[rp];  // basis only (clipped faces)
+        EdgePart me;
+        float iw0, iw1, iw2, w0, w1, w2;
+        if (sp >= 0) {
+            load_slot_edges(T, sp, me);
+            iw0 = T.iw[0][sp]; iw1 = T.iw[1][sp]; iw2 = T.iw[2][sp];
+            w0 = T.w[0][sp]; w1 = T.w[1][sp]; w2 = T.w[2][sp];
+        } else {
+            me = *reinterpret_cast<const EdgePart *>(&rr);
+            iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
+            const FaceData &fdr = fdata_frame[f];
+            w0 = fdr.w[0]; w1 = fdr.w[1]; w2 = fdr.w[2];
+        }
         int64_t Ep[3];
         edge_values(me, i, j, Ep);
         float fEp[3];
@@ -1024,6 +1063,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         // Pass 1 decides ownership (exact integer coverage tests) into 2-bit codes (0 skip, 1 half,
         // 2 whole); pass 2 interpolates and accumulates.  Splitting keeps the coverage tests' and the
         // accumulators' registers apart (occupancy).
+        PHASE_TS(10 + (fEp[0] == 12345.f));
         uint32_t codes = 0;
 #pragma unroll
         for (int dir = 0; dir < 4; ++dir) {
@@ -1065,6 +1105,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
             }
             codes |= code << (2 * dir);
         }
+        PHASE_TS(11 + (codes == 12345u));
 #pragma unroll
         for (int dir = 0; dir < 4; ++dir) {
             const uint32_t code = (codes >> (2 * dir)) & 3u;
@@ -1079,7 +1120,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
             float m[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                const float st = (float)((int64_t)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256 : -256));
+                const float st = (float)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256.0f : -256.0f);  // = (float)(A * 256)
                 m[k] = (2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2);
             }
             float lm[3];
@@ -1130,22 +1171,29 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
     // slot (table full) add straight to global memory
     const int key = rp >= 0 ? rp : -1;
     const int start = run_start(key, lx);
+    // 0/1 multipliers: x += shifted(x) * m is one v_fmac with a DPP operand (exact: m is 0 or 1,
+    // contributions are finite)
+    const float mk1 = lx - 1 >= start ? 1.0f : 0.0f, mk2 = lx - 2 >= start ? 1.0f : 0.0f;
+    const float mk4 = lx - 4 >= start ? 1.0f : 0.0f, mk8 = lx - 8 >= start ? 1.0f : 0.0f;
+    if (!(AB & 32)) {
+        // step-major order: each v_fmac_f32_dpp reads a register written >= NVM-1 instructions
+        // earlier (no DPP read-after-write hazard inside the asm)
+        asm volatile("s_nop 1");  // the accumulators may have been written by the last VALU ops
 #pragma unroll
-    for (int v = 0; v < NVM; ++v) {
-        if (AB & 32) break;
-        float x = acc[v];
-        float y;
-        y = dpp_shr_f<1>(x); if (lx - 1 >= start) x += y;
-        y = dpp_shr_f<2>(x); if (lx - 2 >= start) x += y;
-        y = dpp_shr_f<4>(x); if (lx - 4 >= start) x += y;
-        y = dpp_shr_f<8>(x); if (lx - 8 >= start) x += y;
-        acc[v] = x;
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:1 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk1));
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:2 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk2));
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:4 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk4));
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:8 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk8));
     }
     const int kr = dpp_shl_i<1>(key, -3);
     const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key);
     float *gvb = grad_verts + (int64_t)b * V * 4;
     float *gcb = grad_colors + (int64_t)b * V * C;
     __syncthreads();  // every read of s_G / s_I is done: the union now holds tail partials
+    PHASE_TS(5);
     int q = -1;
     {
         const bool want = tail && sp >= 0;
@@ -1174,6 +1222,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         }
     }
     __syncthreads();
+    PHASE_TS(6);
 
     // ---- phase D: flush.  Thread t handles component t % NV of slot t / NV, so every lane of the
     // workgroup walks one short list in parallel; a slot's components go out as one run of lanes
@@ -1194,6 +1243,10 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
             const int k = (comp_id - 9) / C, c = (comp_id - 9) % C;
             atomicAdd(gcb + (int64_t)T.v[k][slot] * C + c, val);
         }
+    }
+    if (AB & 128) {
+        __syncthreads();
+        PHASE_TS(7);
     }
 }
 
@@ -1423,7 +1476,7 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
         break
     switch (variant) {
         V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);
-        V_GRAD(32); V_GRAD(64); V_GRAD(72);
+        V_GRAD(32); V_GRAD(64); V_GRAD(72); V_GRAD(128);
     default:
         return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: unknown variant");
     }
@@ -1434,6 +1487,15 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     HIP_TRY(hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    return DIRT_OK;
+}
+
+// copy the phase timestamps of the last instrumented backward (variant 128): 10 words per workgroup (8 timestamps, HW_ID, XCC_ID)
+int dirt_debug_read_phase_ts(uint64_t *host, int nwg)
+{
+    if (nwg < 0 || nwg > kTsMaxWG) return fail(DIRT_EINVAL, "dirt_debug_read_phase_ts: bad count");
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_ts), (size_t)nwg * kTsStride * sizeof(uint64_t), 0,
+                                hipMemcpyDeviceToHost));
     return DIRT_OK;
 }
 
