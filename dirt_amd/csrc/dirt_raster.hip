@@ -830,27 +830,44 @@ constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
 constexpr int kHaloPix = kHalo * kHalo;
 constexpr int kSlots = 128;        // distinct records per tile+halo kept in LDS (typ. 10-40)
 constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
+static_assert(kSlots <= 128, "slot ids (0 .. kSlots-1) are stored as int8");
 
 // LDS-resident copy of the edge part of the records seen in a tile + halo (for coverage tests of a
 // neighbour's face) and of their vertex ids (for the flush).
 struct SlotTable {
     int32_t key[kSlots];     // g-buffer word (record index | clipped flag), -1 = free
-    int32_t list[kSlots];    // occupied slots in insertion order
+    int8_t list[kSlots];     // occupied slots in insertion order
     int32_t A[3][kSlots], B[3][kSlots];
-    int64_t C[3][kSlots];
-    uint32_t bx[kSlots], by[kSlots];
+    int32_t e[3][kSlots];      // small records: E + owned at the halo origin pixel (see kGradSmallEdge)
+    uint32_t bx[kSlots], by[kSlots];  // i0 | i1 << 16 (bit 31: large record, use the global Rec)
     int32_t v[3][kSlots];
     float iw[3][kSlots], w[3][kSlots];  // interpolation data of the record (own-pixel path)
     int32_t n;
 };
 
-__device__ __forceinline__ void load_slot_edges(const SlotTable &T, int s, EdgePart &e)
+// A record is "small" for the backward when every |A|, |B| < 2^14 (edges shorter than 64 px).  Such a
+// record is visible somewhere in the 18x18 tile + halo region, so at every region pixel its edge values
+// satisfy |E| < 2^28 (E at a covered pixel) + 2 * 2^14 * 17 * 256 < 2^30: exact in int32, and a
+// coverage test is E0 + A*256*hx + B*256*hy with 24-bit multiplies (hx, hy in 0..17).
+constexpr int32_t kGradSmallEdge = 1 << 14;
+constexpr uint32_t kSlotLarge = 0x80000000u;
+
+__device__ __forceinline__ bool slot_is_large(const SlotTable &T, int s) { return (T.bx[s] & kSlotLarge) != 0; }
+
+// exact coverage of region pixel (hx, hy) = absolute (i, j) by small slot s (bbox + R2/R3 edge test)
+__device__ __forceinline__ bool slot_covers_small(const SlotTable &T, int s, int hx, int hy, int i, int j)
 {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { e.A[k] = T.A[k][s]; e.B[k] = T.B[k][s]; e.C[k] = T.C[k][s]; }
-    e.i0 = (uint16_t)(T.bx[s] & 0xffff); e.i1 = (uint16_t)(T.bx[s] >> 16);
-    e.j0 = (uint16_t)(T.by[s] & 0xffff); e.j1 = (uint16_t)(T.by[s] >> 16);
+    const uint32_t bx = T.bx[s], by = T.by[s];
+    if (i < (int)(bx & 0xffff) || i > (int)((bx >> 16) & 0x7fff) || j < (int)(by & 0xffff) || j > (int)(by >> 16))
+        return false;
+    const int32_t x = hx * 256, y = hy * 256;
+    const int32_t e0 = T.e[0][s] + __mul24(T.A[0][s], x) + __mul24(T.B[0][s], y);
+    const int32_t e1 = T.e[1][s] + __mul24(T.A[1][s], x) + __mul24(T.B[1][s], y);
+    const int32_t e2 = T.e[2][s] + __mul24(T.A[2][s], x) + __mul24(T.B[2][s], y);
+    return min(e0, min(e1, e2)) > 0;
 }
+
+__device__ __forceinline__ int32_t owned_bit(int32_t A, int32_t B) { return (A > 0 || (A == 0 && B < 0)) ? 1 : 0; }
 
 __device__ __forceinline__ int slot_hash(int32_t key) { return (int)(((uint32_t)key * 2654435761u) >> 25) & (kSlots - 1); }
 
@@ -861,7 +878,7 @@ __device__ __forceinline__ int slot_insert(SlotTable &T, int32_t key)
     for (int probe = 0; probe < kSlots; ++probe) {
         const int old = atomicCAS(&T.key[slot], -1, key);
         if (old == -1) {
-            T.list[atomicAdd(&T.n, 1)] = slot;
+            T.list[atomicAdd(&T.n, 1)] = (int8_t)slot;
             return slot;
         }
         if (old == key) return slot;
@@ -898,7 +915,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
     const int C = CC > 0 ? CC : Cdyn;
     const int NV = 9 + 3 * C;
     __shared__ int32_t s_gb[kHaloPix];
-    __shared__ int32_t s_slot[kHaloPix];
+    __shared__ int8_t s_slot[kHaloPix];  // slot of the pixel's record, -1 none, kNoSlot table full
     __shared__ float s_sx[kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), see DESIGN.md 4
     __shared__ float s_sy[kHaloPix];
     // G / I of the staged pixels (phases A-B), then reused for the run-tail partial sums (C-D):
@@ -1008,10 +1025,19 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         const FaceData &fd = fdata_frame[face_of_record(ri, F)];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k]; T.C[k][s] = ep.C[k];
+            T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k];
             T.v[k][s] = fd.v[k];
         }
-        T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16);
+        bool small = true;
+        int64_t E0[3];
+        edge_values(ep, hi0, hj0, E0);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
+                    ep.B[k] < kGradSmallEdge;
+            T.e[k][s] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
+        }
+        T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
         T.by[s] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
         const Rec &r = frame_recs[ri];
 #pragma unroll
@@ -1041,24 +1067,43 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         // vector-memory path (L1-resident: a wave touches a handful of records).
         const int f = face_of_record(rp, F);
         const bool multi = (gp & kGbufMulti) != 0;
-        const Rec &rr = frame_recs[rp];  // basis only (clipped faces)
-        EdgePart me;
+        const Rec &rr = frame_recs[rp];  // large records and the basis of clipped faces
+        const int hx = lx + 1, hy = ly + 1;  // region coordinates of this pixel
+        int32_t mA[3], mB[3], eme[3];       // eme: E + owned here (small records only)
         float iw0, iw1, iw2, w0, w1, w2;
+        float fEp[3];
+        bool me_small;
         if (sp >= 0) {
-            load_slot_edges(T, sp, me);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { mA[k] = T.A[k][sp]; mB[k] = T.B[k][sp]; }
             iw0 = T.iw[0][sp]; iw1 = T.iw[1][sp]; iw2 = T.iw[2][sp];
             w0 = T.w[0][sp]; w1 = T.w[1][sp]; w2 = T.w[2][sp];
+            me_small = !slot_is_large(T, sp);
         } else {
-            me = *reinterpret_cast<const EdgePart *>(&rr);
+            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { mA[k] = me.A[k]; mB[k] = me.B[k]; }
             iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
             const FaceData &fdr = fdata_frame[f];
             w0 = fdr.w[0]; w1 = fdr.w[1]; w2 = fdr.w[2];
+            me_small = false;
         }
-        int64_t Ep[3];
-        edge_values(me, i, j, Ep);
-        float fEp[3];
+        if (me_small) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) fEp[k] = fast_i64_to_f32(Ep[k]);
+            for (int k = 0; k < 3; ++k) {
+                eme[k] = T.e[k][sp] + __mul24(mA[k], hx * 256) + __mul24(mB[k], hy * 256);
+                fEp[k] = (float)(eme[k] - owned_bit(mA[k], mB[k]));
+            }
+        } else {
+            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+            int64_t Ep[3];
+            edge_values(me, i, j, Ep);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                fEp[k] = fast_i64_to_f32(Ep[k]);
+                eme[k] = 0;
+            }
+        }
         // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window).
         // Pass 1 decides ownership (exact integer coverage tests) into 2-bit codes (0 skip, 1 half,
         // 2 whole); pass 2 interpolates and accumulates.  Splitting keeps the coverage tests' and the
@@ -1087,18 +1132,28 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
             } else if (AB & 16) {
                 code = 1u;
             } else {
-                int64_t Eq[3];
+                bool mine_covers_other;
+                if (me_small) {
+                    int32_t e[3];
 #pragma unroll
-                for (int k = 0; k < 3; ++k)
-                    Eq[k] = Ep[k] + (int64_t)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256 : -256);
-                bool mine_covers_other = inside(me, Eq);
+                    for (int k = 0; k < 3; ++k) e[k] = eme[k] + (axis == 0 ? mA[k] : mB[k]) * (me_low ? 256 : -256);
+                    mine_covers_other = min(e[0], min(e[1], e[2])) > 0;
+                } else {
+                    const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+                    int64_t Eq[3];
+                    edge_values(me, i + di, j + dj, Eq);
+                    mine_covers_other = inside(me, Eq);
+                }
                 if (!mine_covers_other && multi)
                     mine_covers_other = covers_face_multi(rp, frame_recs, fdata_frame, F, f, i + di, j + dj);
                 const int sq = s_slot[kq];
-                EdgePart other;
-                if (sq >= 0) load_slot_edges(T, sq, other);
-                else other = *reinterpret_cast<const EdgePart *>(&frame_recs[rq]);
-                bool other_covers_me = edge_covers(other, i, j);
+                bool other_covers_me;
+                if (sq >= 0 && !slot_is_large(T, sq)) {
+                    other_covers_me = slot_covers_small(T, sq, hx, hy, i, j);
+                } else {
+                    const EdgePart other = *reinterpret_cast<const EdgePart *>(&frame_recs[rq]);
+                    other_covers_me = edge_covers(other, i, j);
+                }
                 if (!other_covers_me && (gq & kGbufMulti))
                     other_covers_me = covers_face_multi(rq, frame_recs, fdata_frame, F, fq, i, j);
                 code = (!mine_covers_other && other_covers_me) ? 2u : (mine_covers_other && !other_covers_me) ? 0u : 1u;
@@ -1120,7 +1175,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
             float m[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                const float st = (float)(axis == 0 ? me.A[k] : me.B[k]) * (me_low ? 256.0f : -256.0f);  // = (float)(A * 256)
+                const float st = (float)(axis == 0 ? mA[k] : mB[k]) * (me_low ? 256.0f : -256.0f);  // = (float)(A * 256)
                 m[k] = (2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2);
             }
             float lm[3];
@@ -1139,16 +1194,9 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
                 acc[k * 3 + 2] -= g * ndc;
             }
         }
-    }
-    if (rp >= 0) {
         // colour weights last: keeps their registers out of the pair loop's live range
-        const Rec &rr = frame_recs[rp];
-        const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
-        int64_t Ep[3];
-        edge_values(me, i, j, Ep);
         float lam[3];
-        if (!(AB & 2) && fast_lambda(rr, (gp & kGbufMulti) != 0, fast_i64_to_f32(Ep[0]) * rr.iw[0],
-                                     fast_i64_to_f32(Ep[1]) * rr.iw[1], fast_i64_to_f32(Ep[2]) * rr.iw[2], lam)) {
+        if (!(AB & 2) && fast_lambda(rr, multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
             float Gm[CM];
 #pragma unroll
             for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
