@@ -825,10 +825,13 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
 #ifndef DIRT_GRAD_WAVES
 #define DIRT_GRAD_WAVES 4  // min waves per SIMD the register allocation must allow
 #endif
+#ifndef DIRT_GRAD_ATTR
+#define DIRT_GRAD_ATTR
+#endif
 
 constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
 constexpr int kHaloPix = kHalo * kHalo;
-constexpr int kSlots = 128;        // distinct records per tile+halo kept in LDS (typ. 10-40)
+constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS (typ. 10-40)
 constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
 static_assert(kSlots <= 128, "slot ids (0 .. kSlots-1) are stored as int8");
 
@@ -903,7 +906,7 @@ __device__ __forceinline__ int run_start(int key, int lx)
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
 // 32 skip the DPP run scan (every lane adds into LDS)
 template <int CC, int AB = 0>
-__global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+__global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
                                                    int V, int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
@@ -954,22 +957,45 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         s_ntail = 0;
     }
     const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
-    for (int k = t; k < kHaloPix; k += 256) {
-        const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
-        if (hi < 0 || hj < 0 || hi >= W || hj >= H) {
-            s_gb[k] = -2;
-            continue;
+    {
+        // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * 256)
+        static_assert(kHaloPix <= 512, "two staging passes");
+        int32_t gbv[2];
+        float Gv[2][CM], Iv[2][CM];
+        bool ok[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = t + 256 * u;
+            const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
+            ok[u] = k < kHaloPix && hi >= 0 && hj >= 0 && hi < W && hj < H;
+            gbv[u] = -2;
+            if (ok[u]) {
+                const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
+                gbv[u] = gbuffer[o];
+#pragma unroll
+                for (int c = 0; c < CM; ++c)
+                    if (c < C) {
+                        Gv[u][c] = grad_pixels[o * C + c];
+                        Iv[u][c] = pixels[o * C + c];
+                    }
+            }
         }
-        const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
-        s_gb[k] = gbuffer[o];
-        if (CP == 4 && C == 3) {
-            const float *gp = grad_pixels + o * 3, *ip = pixels + o * 3;
-            *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(gp[0], gp[1], gp[2], 0.0f);
-            *reinterpret_cast<float4 *>(&s_I[k * CP]) = make_float4(ip[0], ip[1], ip[2], 0.0f);
-        } else {
-            for (int c = 0; c < C; ++c) {
-                s_G[k * CP + c] = grad_pixels[o * C + c];
-                s_I[k * CP + c] = pixels[o * C + c];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = t + 256 * u;
+            if (k >= kHaloPix) continue;
+            s_gb[k] = gbv[u];
+            if (!ok[u]) continue;
+            if (CP == 4 && C == 3) {
+                *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(Gv[u][0], Gv[u][1], Gv[u][2], 0.0f);
+                *reinterpret_cast<float4 *>(&s_I[k * CP]) = make_float4(Iv[u][0], Iv[u][1], Iv[u][2], 0.0f);
+            } else {
+#pragma unroll
+                for (int c = 0; c < CM; ++c)
+                    if (c < C) {
+                        s_G[k * CP + c] = Gv[u][c];
+                        s_I[k * CP + c] = Iv[u][c];
+                    }
             }
         }
     }
@@ -1021,30 +1047,26 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
     for (int e = t; e < nslots; e += 256) {
         const int s = T.list[e];
         const int32_t ri = T.key[s] & kGbufIndexMask;
+        // all global loads first (one round trip), then the LDS stores
         const EdgePart ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
-        const FaceData &fd = fdata_frame[face_of_record(ri, F)];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k];
-            T.v[k][s] = fd.v[k];
-        }
+        const FaceData fd = fdata_frame[face_of_record(ri, F)];
+        const Rec &r = frame_recs[ri];
+        const float riw0 = r.iw[0], riw1 = r.iw[1], riw2 = r.iw[2];
         bool small = true;
         int64_t E0[3];
         edge_values(ep, hi0, hj0, E0);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
+            T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k];
+            T.v[k][s] = fd.v[k];
+            T.w[k][s] = fd.w[k];
             small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
                     ep.B[k] < kGradSmallEdge;
             T.e[k][s] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
         }
+        T.iw[0][s] = riw0; T.iw[1][s] = riw1; T.iw[2][s] = riw2;
         T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
         T.by[s] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
-        const Rec &r = frame_recs[ri];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            T.iw[k][s] = r.iw[k];
-            T.w[k][s] = fd.w[k];
-        }
     }
     __syncthreads();
     PHASE_TS(4);
@@ -1262,10 +1284,12 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
             s_next[q] = atomicExch(&s_head[sp], q);
         } else {
             const FaceData &fd = fdata_frame[face_of_record(rp, F)];
-            for (int v = 0; v < NV; ++v) {
-                if (acc[v] == 0.0f) continue;
-                if (v < 9) atomicAdd(gvb + (int64_t)fd.v[v / 3] * 4 + ((v % 3) == 2 ? 3 : v % 3), acc[v]);
-                else atomicAdd(gcb + (int64_t)fd.v[(v - 9) / C] * C + (v - 9) % C, acc[v]);
+            const int32_t vid[3] = {fd.v[0], fd.v[1], fd.v[2]};  // before the atomics (may alias for the compiler)
+#pragma unroll
+            for (int v = 0; v < NVM; ++v) {
+                if (v >= NV || acc[v] == 0.0f) continue;
+                if (v < 9) atomicAdd(gvb + (int64_t)vid[v / 3] * 4 + ((v % 3) == 2 ? 3 : v % 3), acc[v]);
+                else atomicAdd(gcb + (int64_t)vid[(v - 9) / C] * C + (v - 9) % C, acc[v]);
             }
         }
     }
@@ -1281,15 +1305,16 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) void grad_kernel(const float 
         const int e = e0 + t / NV, comp_id = t - (t / NV) * NV;
         if (t >= per_round * NV || e >= n) continue;
         const int slot = T.list[e];
+        const int kv = comp_id < 9 ? comp_id / 3 : (comp_id - 9) / C;
+        const int vid = T.v[kv][slot];
         float val = 0.0f;
         for (int q = s_head[slot]; q >= 0; q = s_next[q]) val += s_part[q * NVM + comp_id];
         if (val == 0.0f) continue;
         if (comp_id < 9) {
-            const int k = comp_id / 3, c3 = comp_id % 3;
-            atomicAdd(gvb + (int64_t)T.v[k][slot] * 4 + (c3 == 2 ? 3 : c3), val);
+            const int c3 = comp_id % 3;
+            atomicAdd(gvb + (int64_t)vid * 4 + (c3 == 2 ? 3 : c3), val);
         } else {
-            const int k = (comp_id - 9) / C, c = (comp_id - 9) % C;
-            atomicAdd(gcb + (int64_t)T.v[k][slot] * C + c, val);
+            atomicAdd(gcb + (int64_t)vid * C + (comp_id - 9) % C, val);
         }
     }
     if (AB & 128) {

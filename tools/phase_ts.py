@@ -75,6 +75,8 @@ def main():
     for name, x in (("B: own record", s10 - b0), ("B: pass 1 (ownership)", s11 - s10), ("B: pass 2..barrier", b5 - s11)):
         print("  %-22s median %8.0f  p90 %8.0f  mean %8.0f ticks  (%.2f us)  [%d WGs]" % (
             name, np.median(x), np.percentile(x, 90), x.mean(), x.mean() * tick_us, ok.sum()))
+    x = ts[:, 12].astype(np.int64) - ts[:, 1].astype(np.int64)
+    print("  %-22s median %8.0f  mean %8.0f ticks  (%.2f us)" % ("A: pair scalars", np.median(x), x.mean(), x.mean() * tick_us))
     life = T[:, 7] - T[:, 0]
     print("  lifetime               median %8.0f  p90 %8.0f ticks  (%.2f us)" % (np.median(life), np.percentile(life, 90),
                                                                             life.mean() * tick_us))
