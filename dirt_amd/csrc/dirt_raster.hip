@@ -874,20 +874,57 @@ __device__ __forceinline__ int32_t owned_bit(int32_t A, int32_t B) { return (A >
 
 __device__ __forceinline__ int slot_hash(int32_t key) { return (int)(((uint32_t)key * 2654435761u) >> 25) & (kSlots - 1); }
 
-// insert `key`, return its slot or kNoSlot if the table is full
-__device__ __forceinline__ int slot_insert(SlotTable &T, int32_t key)
+// Insert `key` for every lane with `want` (called by the whole wave, converged): probes advance in
+// lockstep, and the lanes that created a slot append it to the slot list with one atomic per wave.
+// Returns the slot, kNoSlot if the table is full, -1 where !want.
+__device__ __forceinline__ int slot_insert_wave(SlotTable &T, int32_t key, bool want)
 {
     int slot = slot_hash(key);
+    int result = want ? kNoSlot : -1;
+    bool pending = want, fresh = false;
     for (int probe = 0; probe < kSlots; ++probe) {
-        const int old = atomicCAS(&T.key[slot], -1, key);
-        if (old == -1) {
-            T.list[atomicAdd(&T.n, 1)] = (int8_t)slot;
-            return slot;
+        if (!__any(pending)) break;
+        if (pending) {
+            const int old = atomicCAS(&T.key[slot], -1, key);
+            if (old == -1 || old == key) {
+                result = slot;
+                fresh = old == -1;
+                pending = false;
+            } else {
+                slot = (slot + 1) & (kSlots - 1);
+            }
         }
-        if (old == key) return slot;
-        slot = (slot + 1) & (kSlots - 1);
     }
-    return kNoSlot;
+    const uint64_t mask = __ballot(fresh);
+    if (mask) {
+        int base = 0;
+        if ((threadIdx.x & 63) == 0) base = atomicAdd(&T.n, __popcll(mask));
+        base = __shfl(base, 0, 64);
+        if (fresh)
+            T.list[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = (int8_t)result;
+    }
+    return result;
+}
+
+// pair scalar s = -0.5 sum_c (G(p)+G(q)) (I(q)-I(p)) of staged pixels p = k, q = k2 (same operand order
+// as the oracle), 0 when either is outside the frame; every operand read unconditionally (no branches
+// between the LDS reads)
+template <int CP, int CM>
+__device__ __forceinline__ float pair_scalar(const int32_t *s_gb, const float *s_G, const float *s_I, int k, int k2, int C)
+{
+    const int32_t g1 = s_gb[k], g2 = s_gb[k2];
+    float a = 0.0f;
+    if (CP == 4 && CM == 3) {
+        const float4 Gp = *reinterpret_cast<const float4 *>(&s_G[k * 4]), Gq = *reinterpret_cast<const float4 *>(&s_G[k2 * 4]);
+        const float4 Ip = *reinterpret_cast<const float4 *>(&s_I[k * 4]), Iq = *reinterpret_cast<const float4 *>(&s_I[k2 * 4]);
+        a = (Gp.x + Gq.x) * (Iq.x - Ip.x);
+        a = a + (Gp.y + Gq.y) * (Iq.y - Ip.y);
+        a = a + (Gp.z + Gq.z) * (Iq.z - Ip.z);
+    } else {
+        for (int c = 0; c < C; ++c) a += (s_G[k * CP + c] + s_G[k2 * CP + c]) * (s_I[k2 * CP + c] - s_I[k * CP + c]);
+    }
+    return (g1 != -2 && g2 != -2) ? -0.5f * a : 0.0f;
 }
 
 // Index (0..15) of the first lane of this lane's run of equal `key` in its 16-lane DPP row.
@@ -1003,70 +1040,73 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     PHASE_TS(1);
     const int32_t gp = in_frame ? s_gb[kme] : -2;
     {
-        // pair scalars for pairs starting at a staged pixel (same operand order as the oracle)
-        for (int k = t; k < kHaloPix; k += 256) {
-            const int hx = k % kHalo, hy = k / kHalo;
-            float sx = 0.0f, sy = 0.0f;
-            if (s_gb[k] != -2) {
-                if (hx + 1 < kHalo && s_gb[k + 1] != -2) {
-                    float a = 0.0f;
-                    for (int c = 0; c < C; ++c)
-                        a += (s_G[k * CP + c] + s_G[(k + 1) * CP + c]) * (s_I[(k + 1) * CP + c] - s_I[k * CP + c]);
-                    sx = -0.5f * a;
-                }
-                if (hy + 1 < kHalo && s_gb[k + kHalo] != -2) {
-                    float a = 0.0f;
-                    for (int c = 0; c < C; ++c)
-                        a += (s_G[k * CP + c] + s_G[(k + kHalo) * CP + c]) * (s_I[(k + kHalo) * CP + c] - s_I[k * CP + c]);
-                    sy = -0.5f * a;
-                }
-            }
-            s_sx[k] = sx;
-            s_sy[k] = sy;
-        }
-        // own pixels first (run heads only; all 256 distinct keys may not fit: the rest read global
-        // memory), then the halo ring
+        const int rt = (t & 63) * 4 + (t >> 6);  // 0..255 spread over the four waves
+        // own pixels first (run heads only; all distinct keys may not fit: the rest read global memory),
+        // then the 68 halo ring pixels
         const int32_t g = s_gb[kme];
         const int key = g >= 0 ? g : -1;
         const int start = run_start(key, lx);
-        int slot = -1;
-        if (key >= 0 && start == lx) slot = slot_insert(T, key);
+        int slot = slot_insert_wave(T, key, key >= 0 && start == lx);
         slot = __shfl(slot, (t & 48) + start, 64);
         s_slot[kme] = key >= 0 ? slot : -1;
-        for (int k = t; k < kHaloPix; k += 256) {
-            const int hx = k % kHalo, hy = k / kHalo;
-            if (hx != 0 && hy != 0 && hx != kHalo - 1 && hy != kHalo - 1) continue;
-            const int32_t g = s_gb[k];
-            s_slot[k] = g >= 0 ? slot_insert(T, g) : -1;
-        }
+        int kr = -1;
+        if (rt < 18) kr = rt;                                      // bottom row
+        else if (rt < 36) kr = (kHalo - 1) * kHalo + (rt - 18);    // top row
+        else if (rt < 52) kr = (rt - 35) * kHalo;                  // left column (rows 1..16)
+        else if (rt < 68) kr = (rt - 51) * kHalo + kHalo - 1;      // right column
+        const int32_t gr = kr >= 0 ? s_gb[kr] : -1;
+        const int sr = slot_insert_wave(T, gr, gr >= 0);
+        if (kr >= 0) s_slot[kr] = gr >= 0 ? sr : -1;
     }
     __syncthreads();
     PHASE_TS(2);
     PHASE_TS(3);
     const int nslots = T.n;
-    for (int e = t; e < nslots; e += 256) {
-        const int s = T.list[e];
-        const int32_t ri = T.key[s] & kGbufIndexMask;
-        // all global loads first (one round trip), then the LDS stores
-        const EdgePart ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
-        const FaceData fd = fdata_frame[face_of_record(ri, F)];
-        const Rec &r = frame_recs[ri];
-        const float riw0 = r.iw[0], riw1 = r.iw[1], riw2 = r.iw[2];
-        bool small = true;
-        int64_t E0[3];
-        edge_values(ep, hi0, hj0, E0);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            T.A[k][s] = ep.A[k]; T.B[k][s] = ep.B[k];
-            T.v[k][s] = fd.v[k];
-            T.w[k][s] = fd.w[k];
-            small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
-                    ep.B[k] < kGradSmallEdge;
-            T.e[k][s] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
+    static_assert(kSlots <= 256, "one slot per thread");
+    {
+        // slot fill: the record loads are issued first and land while the pair scalars are computed
+        const bool filler = t < nslots;
+        int sf = 0;
+        EdgePart ep{};
+        FaceData fd{};
+        float riw0 = 0.f, riw1 = 0.f, riw2 = 0.f;
+        if (filler) {
+            sf = T.list[t];
+            const int32_t ri = T.key[sf] & kGbufIndexMask;
+            ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
+            fd = fdata_frame[face_of_record(ri, F)];
+            const Rec &r = frame_recs[ri];
+            riw0 = r.iw[0]; riw1 = r.iw[1]; riw2 = r.iw[2];
         }
-        T.iw[0][s] = riw0; T.iw[1][s] = riw1; T.iw[2][s] = riw2;
-        T.bx[s] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
-        T.by[s] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
+        // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
+        // bottom row of the halo (their one pair into the tile); nothing reads the others
+        const int rt = (t & 63) * 4 + (t >> 6);
+        s_sx[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + 1, C);
+        s_sy[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + kHalo, C);
+        if (rt < 16) {
+            const int k = (rt + 1) * kHalo;  // (0, rt + 1)
+            s_sx[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + 1, C);
+        } else if (rt < 32) {
+            const int k = rt - 15;  // (rt - 15, 0)
+            s_sy[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + kHalo, C);
+        }
+        if (filler) {
+            bool small = true;
+            int64_t E0[3];
+            edge_values(ep, hi0, hj0, E0);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                T.A[k][sf] = ep.A[k]; T.B[k][sf] = ep.B[k];
+                T.v[k][sf] = fd.v[k];
+                T.w[k][sf] = fd.w[k];
+                small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
+                        ep.B[k] < kGradSmallEdge;
+                T.e[k][sf] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
+            }
+            T.iw[0][sf] = riw0; T.iw[1][sf] = riw1; T.iw[2][sf] = riw2;
+            T.bx[sf] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
+            T.by[sf] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
+        }
     }
     __syncthreads();
     PHASE_TS(4);
