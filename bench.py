@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="steps captured per HIP graph (each replay runs that many complete steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--profile-steps", type=int, default=50)
@@ -115,14 +117,21 @@ def main():
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    # the timed loop runs exactly args.steps complete steps: full graph replays of gs steps each, the
+    # remainder eagerly
+    gs = 1 if args.no_graph else max(1, min(args.graph_steps, args.steps))
+    n_replays, n_rest = divmod(args.steps, gs)
     run = step
     if not args.no_graph:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            step()
-        for _ in range(3):
+            for _ in range(gs):
+                step()
+        for _ in range(2):
             graph.replay()
         run = graph.replay
+    else:
+        n_replays, n_rest = args.steps, 0
 
     def barrier():
         if world > 1:
@@ -131,8 +140,10 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(n_replays):
         run()
+    for _ in range(n_rest):
+        step()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -173,7 +184,7 @@ def main():
                                    (args.config, B, F, _r, H, W, C),
                        "frames_per_rank": B, "height": H, "width": W, "channels": C, "faces": F, "vertices": V,
                        "parallelism": "frames sharded over %d rank(s), no collective in step" % world,
-                       "hip_graph": not args.no_graph},
+                       "hip_graph": not args.no_graph, "steps_per_graph": gs},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels_us": {k: round(u, 2) for k, u in kern_us.items()},

@@ -98,7 +98,7 @@ struct Layout {
     int nctx, ncty, ncoarse;  // coarse tiles per frame (<= kMaxCoarse)
     int64_t nrec;
     size_t saved_recs, saved_fdata, saved_total;
-    size_t off_count, off_cursor, off_offset, off_flag, off_bins, scratch_total;
+    size_t off_count, off_cursor, off_done, off_offset, off_flag, off_bins, scratch_total;
     int64_t bin_capacity;
 };
 
@@ -135,6 +135,7 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     size_t o = 0;
     L.off_count = o;  o += (size_t)align_up(nc * 4, 256);
     L.off_cursor = o; o += (size_t)align_up(nc * 4, 256);
+    L.off_done = o;   o += 256;  // setup's finished-block ticket (zeroed with the counts)
     L.off_offset = o; o += (size_t)align_up(nc * 8, 256);
     L.off_flag = o;   o += 256;
     L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 8, 256);
@@ -239,11 +240,72 @@ __device__ __forceinline__ void load_bbox(const Rec &r, uint32_t &bx, uint32_t &
     by = q.y;
 }
 
+constexpr int kScanThreads = 1024;
+constexpr int kScanPerThread = 4;
+
+// exclusive prefix sum of the bin counts (uint32) into bin offsets (uint64) by one workgroup of NT
+// threads; counts are read with agent-scope atomic loads (they were produced by other workgroups'
+// atomics in the same launch when called from setup_kernel)
+template <int NT>
+__device__ void scan_counts(const uint32_t *in, uint64_t *__restrict__ out, int64_t n)
+{
+    __shared__ uint64_t wave_sums[NT / 64];
+    __shared__ uint64_t carry_s;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint64_t carry = 0;
+    for (int64_t base = 0; base < n; base += (int64_t)NT * kScanPerThread) {
+        const int64_t k0 = base + (int64_t)t * kScanPerThread;
+        uint32_t v[kScanPerThread];
+        uint64_t local = 0;
+#pragma unroll
+        for (int q = 0; q < kScanPerThread; ++q)
+            v[q] = (k0 + q < n) ? __hip_atomic_load(in + k0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+        for (int q = 0; q < kScanPerThread; ++q) local += v[q];
+        uint64_t x = local;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wave_sums[wave] = x;
+        __syncthreads();
+        if (wave == 0) {
+            uint64_t w = lane < NT / 64 ? wave_sums[lane] : 0;
+#pragma unroll
+            for (int d = 1; d < NT / 64; d <<= 1) {
+                const uint64_t y = __shfl_up(w, d, 64);
+                if (lane >= d) w += y;
+            }
+            if (lane < NT / 64) wave_sums[lane] = w;
+            if (lane == NT / 64 - 1) carry_s = w;
+        }
+        __syncthreads();
+        uint64_t run = carry + (wave > 0 ? wave_sums[wave - 1] : 0) + (x - local);
+#pragma unroll
+        for (int q = 0; q < kScanPerThread; ++q) {
+            if (k0 + q < n) out[k0 + q] = run;
+            run += v[q];
+        }
+        carry += carry_s;
+        __syncthreads();
+    }
+}
+
+// stand-alone scan (frames without faces: setup_kernel is not launched)
+__global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                            int64_t n)
+{
+    scan_counts<kScanThreads>(in, out, n);
+}
+
 __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restrict__ verts,
                                                             const int32_t *__restrict__ faces, int V, int F, int W,
                                                             int H, int cshift, int nctx, int ncoarse, int64_t nrec,
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
-                                                            uint32_t *__restrict__ ccount, uint32_t *__restrict__ flag)
+                                                            uint32_t *__restrict__ ccount, uint32_t *__restrict__ flag,
+                                                            uint32_t *__restrict__ done, uint64_t *__restrict__ coffset,
+                                                            int64_t nc)
 {
     __shared__ uint32_t hist[kMaxCoarse];
     const int b = blockIdx.y, t = threadIdx.x;
@@ -320,65 +382,26 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     }
     __syncthreads();
     uint32_t *cc = ccount + (int64_t)b * ncoarse;
+    // count atomics WITH return: a returned value means the add has been performed at the coherence
+    // point, so after the barrier this block's counts are all in before its ticket (no release fence,
+    // which would write back the whole L2)
+    uint32_t sink = 0;
     for (int c = t; c < ncoarse; c += kBinThreads)
-        if (hist[c]) atomicAdd(&cc[c], hist[c]);
+        if (hist[c]) sink |= atomicAdd(&cc[c], hist[c]);
+    __shared__ uint32_t s_ticket;
+    if (sink == 0xffffffffu) s_ticket = 0;  // consume the returns (never true in practice)
+    __syncthreads();
+    // the last block to take a ticket turns the counts into bin offsets (saves a dependent scan
+    // launch); it reads the counts with agent-scope atomic loads
+    if (t == 0) s_ticket = atomicAdd(done, 1u);
+    __syncthreads();
+    if (s_ticket != gridDim.x * gridDim.y - 1) return;
+    scan_counts<kBinThreads>(ccount, coffset, nc);
 }
 
 // ------------------------------------------------------------------------------------------------
 // K2: exclusive scan of the per-coarse-tile counts (one workgroup; B*ncoarse is 256 per 1024^2 frame)
 
-constexpr int kScanThreads = 1024;
-constexpr int kScanPerThread = 4;
-
-__global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                            int64_t n)
-{
-    __shared__ uint64_t wave_sums[kScanThreads / 64];
-    __shared__ uint64_t carry_s;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint64_t carry = 0;
-    for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kScanPerThread) {
-        const int64_t k0 = base + (int64_t)t * kScanPerThread;
-        uint32_t v[kScanPerThread];
-        uint64_t local = 0;
-        if (k0 + kScanPerThread <= n) {
-            const uint4 q = *reinterpret_cast<const uint4 *>(in + k0);
-            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-        } else {
-#pragma unroll
-            for (int q = 0; q < kScanPerThread; ++q) v[q] = (k0 + q < n) ? in[k0 + q] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < kScanPerThread; ++q) local += v[q];
-        uint64_t x = local;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) wave_sums[wave] = x;
-        __syncthreads();
-        if (wave == 0) {
-            uint64_t w = lane < kScanThreads / 64 ? wave_sums[lane] : 0;
-#pragma unroll
-            for (int d = 1; d < kScanThreads / 64; d <<= 1) {
-                const uint64_t y = __shfl_up(w, d, 64);
-                if (lane >= d) w += y;
-            }
-            if (lane < kScanThreads / 64) wave_sums[lane] = w;
-            if (lane == kScanThreads / 64 - 1) carry_s = w;
-        }
-        __syncthreads();
-        uint64_t run = carry + (wave > 0 ? wave_sums[wave - 1] : 0) + (x - local);
-#pragma unroll
-        for (int q = 0; q < kScanPerThread; ++q) {
-            if (k0 + q < n) out[k0 + q] = run;
-            run += v[q];
-        }
-        carry += carry_s;
-        __syncthreads();
-    }
-}
 
 // ------------------------------------------------------------------------------------------------
 // K3: fill the coarse bins.  Entry = {record index, bbox clamped to the coarse tile, 8 bits per side}.
@@ -471,6 +494,15 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
 // Results are bit-identical to R3/R4 (oracle) by construction.
 
 constexpr int kStrips = 4;
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 shares an L2),
+// so give each residue class a contiguous band of tiles; neighbouring tiles then share halo pixels and
+// records in one L2.  A bijection on [0, n); speed only, never correctness.
+__device__ __forceinline__ int xcd_tile(int x, int n)
+{
+    const int q = n >> 3, r = n & 7, g = x & 7, k = x >> 3;
+    return g * q + min(g, r) + k;
+}
+
 constexpr int kSmallEdge = 1 << 16;
 constexpr int kListCap = 256;      // per-wave survivor list (filtered record indices)
 constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per round (2 loads per lane in flight)
@@ -587,7 +619,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const int C = CC > 0 ? CC : Cdyn;
     __shared__ int32_t s_list_all[kStrips][kListCap];
     __shared__ StripEntry s_ent_all[kStrips][64];
-    const int tile = blockIdx.x, b = blockIdx.y;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
     const int t = threadIdx.x, lx = t & 15, ly = t >> 4, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -971,7 +1003,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     __shared__ int32_t s_next[kTailCap];
     __shared__ int32_t s_ntail;
 
-    const int tile = blockIdx.x, b = blockIdx.y;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
     const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
     const int i = tx * kTile + lx, j = ty * kTile + ly;
@@ -1381,6 +1413,28 @@ __global__ __launch_bounds__(256) void zero2_kernel(float *__restrict__ a, int64
     }
 }
 
+// PMC calibration (tools/pmc_calibrate.py): read `n` elements of W bytes once each, coalesced, with the
+// access widths the product kernels use, so FETCH_SIZE can be converted to bytes per width
+template <int W>
+__global__ __launch_bounds__(256) void read_bytes_kernel(const char *__restrict__ src, int64_t n, float *out)
+{
+    float acc = 0.0f;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const char *p = src + e * W;
+        if (W == 4) acc += *reinterpret_cast<const float *>(p);
+        if (W == 12) {
+            const float *q = reinterpret_cast<const float *>(p);
+            acc += q[0] + q[1] + q[2];
+        }
+        if (W == 16) {
+            const float4 q = *reinterpret_cast<const float4 *>(p);
+            acc += q.x + q.y + q.z + q.w;
+        }
+    }
+    if (acc == 1.2345e-30f) out[0] = acc;  // keep the loads
+}
+
 __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n, int V, uint32_t *flag)
 {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
@@ -1435,6 +1489,7 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
     uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
     uint32_t *ccursor = reinterpret_cast<uint32_t *>(sc + L.off_cursor);
+    uint32_t *done = reinterpret_cast<uint32_t *>(sc + L.off_done);
     uint64_t *coffset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
     uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
     uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
@@ -1446,14 +1501,14 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     if (F > 0) {
         ProfScope ps(K_SETUP, stream);
         setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
-                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag);
+                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag,
+                                                                 done, coffset, nc);
         HIP_TRY(hipGetLastError());
-    }
-    {
+    } else {
         ProfScope ps(K_SCAN, stream);
         scan_kernel<<<dim3(1), dim3(kScanThreads), 0, stream>>>(ccount, coffset, nc);
+        HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipGetLastError());
     if (F > 0) {
         ProfScope ps(K_FILL, stream);
         fill_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(recs, fdata, F, L.cshift, L.nctx, L.ncoarse, L.nrec,
@@ -1600,6 +1655,19 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     HIP_TRY(hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    return DIRT_OK;
+}
+
+int dirt_debug_read_bytes(int width, const void *src, size_t bytes, float *out, void *stream_)
+{
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    if (width != 4 && width != 12 && width != 16) return fail(DIRT_EINVAL, "dirt_debug_read_bytes: width 4, 12 or 16");
+    const int64_t n = (int64_t)(bytes / (size_t)width);
+    const dim3 grid(2048), block(256);
+    if (width == 4) read_bytes_kernel<4><<<grid, block, 0, stream>>>(static_cast<const char *>(src), n, out);
+    if (width == 12) read_bytes_kernel<12><<<grid, block, 0, stream>>>(static_cast<const char *>(src), n, out);
+    if (width == 16) read_bytes_kernel<16><<<grid, block, 0, stream>>>(static_cast<const char *>(src), n, out);
+    HIP_TRY(hipGetLastError());
     return DIRT_OK;
 }
 
