@@ -20,17 +20,24 @@ SHADER_OCEANIC_HORIZON = 1
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
+ABI_VERSION = 3
+
+FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
+BWD_ACCUMULATE = 1     # dirt_rasterise_bwd flags
 
 # every symbol include/dirt_mi355x.h declares, with its ctypes signature
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _I64 = ctypes.c_int64
 _SZ = ctypes.c_size_t
+_U = ctypes.c_uint
 SIGNATURES = {
     "dirt_abi_version": (_I, []),
     "dirt_workspace_sizes": (_I, [_I, _I, _I, _I, _I, _I, _I64, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
-    "dirt_rasterise_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _P]),
-    "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "dirt_rasterise_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _U,
+                                _P, _P, _P]),
+    "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _U, _P]),
+    "dirt_scratch_clear": (_I, [_I, _I, _I, _I, _I64, _P, _SZ, _P]),
     "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
     "dirt_profile_enable": (_I, [_I]),
     "dirt_profile_read": (_I, [_I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double)]),
@@ -57,6 +64,9 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.dirt_abi_version() != ABI_VERSION:
+        raise ImportError("%s has ABI version %d, this binding expects %d: rebuild with `make`"
+                          % (LIB_PATH, lib.dirt_abi_version(), ABI_VERSION))
     _lib = lib
     return lib
 

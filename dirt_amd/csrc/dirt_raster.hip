@@ -136,7 +136,7 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.off_count = o;  o += (size_t)align_up(nc * 4, 256);
     L.off_cursor = o; o += (size_t)align_up(nc * 4, 256);
     L.off_done = o;   o += 256;  // setup's finished-block ticket (zeroed with the counts)
-    L.off_offset = o; o += (size_t)align_up(nc * 8, 256);
+    L.off_offset = o; o += (size_t)align_up((nc + 1) * 8, 256);
     L.off_flag = o;   o += 256;
     L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 8, 256);
     L.scratch_total = o;
@@ -290,6 +290,7 @@ __device__ void scan_counts(const uint32_t *in, uint64_t *__restrict__ out, int6
         carry += carry_s;
         __syncthreads();
     }
+    if (t == 0) out[n] = carry;  // n + 1 offsets: bin k holds [out[k], out[k+1])
 }
 
 // stand-alone scan (frames without faces: setup_kernel is not launched)
@@ -448,11 +449,19 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
                                                            int nctx, int ncoarse, int64_t nrec,
                                                            const uint64_t *__restrict__ coffset,
                                                            uint32_t *__restrict__ ccursor, uint2 *__restrict__ bins,
-                                                           int64_t capacity)
+                                                           int64_t capacity, uint32_t *__restrict__ ccount,
+                                                           uint32_t *__restrict__ done, int64_t nc)
 {
     __shared__ uint32_t hist[kMaxCoarse];
     __shared__ uint64_t base[kMaxCoarse];
     const int b = blockIdx.y, t = threadIdx.x;
+    {
+        // self-cleaning scratch: nothing reads the counts after setup's scan (the raster uses offset
+        // differences), so they and setup's ticket are returned to zero here for the next forward
+        const int64_t nblk = (int64_t)gridDim.x * gridDim.y, blk = (int64_t)b * gridDim.x + blockIdx.x;
+        for (int64_t k = blk * kBinThreads + t; k < nc; k += nblk * kBinThreads) ccount[k] = 0;
+        if (blk == 0 && t == 0) *done = 0;
+    }
     for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
     __syncthreads();
     const Rec *frame_recs = recs + (int64_t)b * nrec;
@@ -608,13 +617,31 @@ __device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
 template <int CC, int AB = 0>
 __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
-                                                     const uint32_t *__restrict__ ccount,
+                                                     uint32_t *__restrict__ ccursor,
                                                      const uint64_t *__restrict__ coffset,
                                                      const uint2 *__restrict__ bins, int64_t capacity,
                                                      int B, int H, int W, int Cdyn, int V, int F, int ntx, int cshift,
                                                      int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
-                                                     int32_t *__restrict__ gbuffer)
+                                                     int32_t *__restrict__ gbuffer, float *__restrict__ zero_a,
+                                                     int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b)
 {
+    if (!(AB & 16)) {
+        // housekeeping spread over all blocks (a few KB each): return fill's bin cursors to zero for
+        // the next forward, and zero-fill the caller's gradient accumulators if it passed them
+        const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
+        const int64_t gt = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x, gs = nblk * 256;
+        const int64_t nc = (int64_t)B * ncoarse;
+        for (int64_t k = gt; k < nc; k += gs) ccursor[k] = 0;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (zero_a) {
+            for (int64_t k = gt; k < (nzero_a >> 2); k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
+            for (int64_t k = (nzero_a & ~3LL) + gt; k < nzero_a; k += gs) zero_a[k] = 0.f;
+        }
+        if (zero_b) {
+            for (int64_t k = gt; k < (nzero_b >> 2); k += gs) reinterpret_cast<float4 *>(zero_b)[k] = z4;
+            for (int64_t k = (nzero_b & ~3LL) + gt; k < nzero_b; k += gs) zero_b[k] = 0.f;
+        }
+    }
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     const int C = CC > 0 ? CC : Cdyn;
     __shared__ int32_t s_list_all[kStrips][kListCap];
@@ -645,8 +672,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const int cx = si0 >> cshift, cy = sj0 >> cshift;
     const int c = cy * nctx + cx;
     const int64_t cc = (int64_t)b * ncoarse + c;
-    const uint32_t cnt = ccount[cc];
     const uint64_t off = coffset[cc];
+    const uint32_t cnt = (uint32_t)(coffset[cc + 1] - off);
     // strip rectangle relative to the coarse tile
     const uint32_t rx0 = (uint32_t)(si0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
     const uint32_t ry0 = (uint32_t)(sj0 - (cy << cshift)), ry1 = ry0 + 3;
@@ -1055,7 +1082,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             if (k >= kHaloPix) continue;
             s_gb[k] = gbv[u];
             if (!ok[u]) continue;
-            if (CP == 4 && C == 3) {
+            if constexpr (CM == 3) {
                 *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(Gv[u][0], Gv[u][1], Gv[u][2], 0.0f);
                 *reinterpret_cast<float4 *>(&s_I[k * CP]) = make_float4(Iv[u][0], Iv[u][1], Iv[u][2], 0.0f);
             } else {
@@ -1448,7 +1475,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 2; }
+int dirt_abi_version(void) { return 3; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -1468,7 +1495,8 @@ int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_c
 int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
                        const int32_t *faces, const float *camera_pos, int B, int H, int W, int C, int V, int F,
                        int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch,
-                       size_t scratch_bytes, int64_t bin_capacity, void *stream_)
+                       size_t scratch_bytes, int64_t bin_capacity, unsigned flags, float *zero_grad_vertices,
+                       float *zero_grad_vertex_colors, void *stream_)
 {
     (void)camera_pos;
     int rc = validate(B, H, W, C, V, F);
@@ -1488,15 +1516,16 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
     FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
     uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
-    uint32_t *ccursor = reinterpret_cast<uint32_t *>(sc + L.off_cursor);
+    uint32_t *ccursor = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_cursor);
     uint32_t *done = reinterpret_cast<uint32_t *>(sc + L.off_done);
     uint64_t *coffset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
     uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
     uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
     const int64_t nc = (int64_t)B * L.ncoarse;
 
-    // counts and cursors are adjacent: one memset
-    HIP_TRY(hipMemsetAsync(ccount, 0, L.off_offset - L.off_count, stream));
+    // counts, cursors and the setup ticket are adjacent: one memset, unless the caller vouches that
+    // they are zero (DIRT_FWD_SCRATCH_CLEAN, e.g. cleared by dirt_scratch_clear on a side stream)
+    if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_offset - L.off_count, stream));
     const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     if (F > 0) {
         ProfScope ps(K_SETUP, stream);
@@ -1512,15 +1541,18 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     if (F > 0) {
         ProfScope ps(K_FILL, stream);
         fill_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(recs, fdata, F, L.cshift, L.nctx, L.ncoarse, L.nrec,
-                                                                coffset, ccursor, bins, L.bin_capacity);
+                                                                coffset, ccursor, bins, L.bin_capacity, ccount, done, nc);
         HIP_TRY(hipGetLastError());
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
 #define LAUNCH_RASTER(CC)                                                                                        \
-    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, coffset,    \
+    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,   \
                                                       bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift,    \
-                                                      L.nctx, L.ncoarse, L.nrec, pixels, gbuffer)
+                                                      L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices, \
+                                                      zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
+                                                      zero_grad_vertex_colors,                                     \
+                                                      zero_grad_vertex_colors ? (int64_t)B * V * C : 0)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else LAUNCH_RASTER(0);
@@ -1532,7 +1564,7 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
 int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces, const float *pixels,
                        const float *grad_pixels, const int32_t *gbuffer, const void *saved, int B, int H, int W, int C,
                        int V, int F, float *grad_vertices, float *grad_vertex_colors, float *grad_background,
-                       void *stream_)
+                       unsigned flags, void *stream_)
 {
     // vertices / vertex_colors / faces are part of the contract (rasterise_grad_common.h:19-24); the
     // forward's FaceData in `saved` already holds what the kernel needs from them.
@@ -1552,7 +1584,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     const char *sv = static_cast<const char *>(saved);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
-    if (V > 0) {
+    if (V > 0 && !(flags & DIRT_BWD_ACCUMULATE)) {
         const int64_t na = (int64_t)B * V * 4, nb = (int64_t)B * V * C;
         const int64_t blocks = std::min<int64_t>(2048, (na / 4 + 255) / 256 + 1);
         zero2_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(grad_vertices, na, grad_vertex_colors, nb);
@@ -1586,7 +1618,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     const char *sv = static_cast<const char *>(saved), *sc = static_cast<const char *>(scratch);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
-    const uint32_t *ccount = reinterpret_cast<const uint32_t *>(sc + L.off_count);
+    uint32_t *ccursor = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_cursor);
     const uint64_t *coffset = reinterpret_cast<const uint64_t *>(sc + L.off_offset);
     const uint2 *bins = reinterpret_cast<const uint2 *>(sc + L.off_bins);
     hipEvent_t e0, e1;
@@ -1596,9 +1628,10 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
 #define V_RAST(AB)                                                                                                 \
     case AB:                                                                                                       \
-        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, coffset, \
+        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,\
                                                              bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift, \
-                                                             L.nctx, L.ncoarse, L.nrec, pixels, gbuffer);          \
+                                                             L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, 0,  \
+                                                             nullptr, 0);                                           \
         break
     switch (variant) {
         V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8);
@@ -1706,6 +1739,22 @@ int dirt_profile_read(int kernel_id, const char **name, int *launches, double *t
     if (name) *name = kKernelNames[kernel_id];
     if (launches) *launches = (int)g_prof.ev[kernel_id].size();
     if (total_ms) *total_ms = tot;
+    return DIRT_OK;
+}
+
+int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *scratch, size_t scratch_bytes,
+                       void *stream_)
+{
+    if (B < 0 || F < 0 || H <= 0 || W <= 0 || H > DIRT_MAX_DIM || W > DIRT_MAX_DIM)
+        return fail(DIRT_EINVAL, "dirt_scratch_clear: bad sizes");
+    if (B == 0) return DIRT_OK;
+    Layout L;
+    const int rc = make_layout(B, H, W, F, bin_capacity, L);
+    if (rc) return rc;
+    if (!scratch || scratch_bytes < L.scratch_total)
+        return fail(DIRT_EINVAL, "dirt_scratch_clear: scratch smaller than dirt_workspace_sizes()");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    HIP_TRY(hipMemsetAsync(static_cast<char *>(scratch) + L.off_count, 0, L.off_offset - L.off_count, stream));
     return DIRT_OK;
 }
 

@@ -61,7 +61,8 @@ class _RasteriseFunction(torch.autograd.Function):
             _lib.check(lib.dirt_rasterise_fwd(
                 background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
                 B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
-                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, stream))
+                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, 0, None, None,
+                stream))
         ctx.save_for_backward(vertices, vertex_colors, faces, pixels, gbuffer, saved)
         ctx.dims = (B, H, W, C, V, F)
         ctx.shader_id = shader_id
@@ -86,7 +87,7 @@ class _RasteriseFunction(torch.autograd.Function):
                 vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), pixels.data_ptr(),
                 grad_pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(),
                 B, H, W, C, V, F, grad_vertices.data_ptr(), grad_colors.data_ptr(), grad_background.data_ptr(),
-                stream))
+                0, stream))
         return grad_background, grad_vertices, grad_colors, None, None, None, None, None, None, None
 
 

@@ -5,6 +5,12 @@ that is the drop-in surface.  A serving or training loop that renders the same s
 instead hold a `RasteriseSession`: buffers are allocated once and each call is a single ctypes call into
 the C ABI, so a whole forward+backward step can be captured into a HIP graph (torch.cuda.CUDAGraph) and
 replayed without host launch overhead.  Results are identical to the autograd path (same kernels).
+
+The session also removes the per-step housekeeping launches: the scratch is zero-filled once and every
+forward leaves it clean (DIRT_FWD_SCRATCH_CLEAN skips the forward's clearing memset), and the forward's
+raster kernel zero-fills the gradient accumulators in passing, so the backward adds into them
+(DIRT_BWD_ACCUMULATE) without a clearing kernel of its own.  Hence: the gradients returned by
+`backward` stay valid until the next `forward`, and each forward is followed by at most one backward.
 """
 import torch
 
@@ -29,6 +35,7 @@ class RasteriseSession:
         self.grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         self._lib = _lib.load()
         self._inputs = None
+        self.scratch.zero_()  # clean once; every forward leaves it clean
 
     def _check(self, t, shape, dtype):
         if t.device != self.device or t.dtype != dtype or tuple(t.shape) != shape or not t.is_contiguous():
@@ -48,7 +55,8 @@ class RasteriseSession:
             background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
             B, H, W, C, V, F, self.shader_id, self.pixels.data_ptr(), self.gbuffer.data_ptr(),
             self.saved.data_ptr(), self.saved_bytes, self.scratch.data_ptr(), self.scratch_bytes,
-            self.bin_capacity, stream))
+            self.bin_capacity, _lib.FWD_SCRATCH_CLEAN, self.grad_vertices.data_ptr(),
+            self.grad_vertex_colors.data_ptr(), stream))
         return self.pixels
 
     def backward(self, grad_pixels):
@@ -62,5 +70,5 @@ class RasteriseSession:
             vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), self.pixels.data_ptr(),
             grad_pixels.data_ptr(), self.gbuffer.data_ptr(), self.saved.data_ptr(), B, H, W, C, V, F,
             self.grad_vertices.data_ptr(), self.grad_vertex_colors.data_ptr(), self.grad_background.data_ptr(),
-            stream))
+            _lib.BWD_ACCUMULATE, stream))
         return self.grad_background, self.grad_vertices, self.grad_vertex_colors

@@ -71,16 +71,32 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
                        int B, int H, int W, int C, int V, int F, int shader_id,
                        float *pixels, int32_t *gbuffer,
                        void *saved, size_t saved_bytes, void *scratch, size_t scratch_bytes,
-                       int64_t bin_capacity, void *stream);
+                       int64_t bin_capacity, unsigned flags,
+                       float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream);
+/* flags of dirt_rasterise_fwd.  Every forward returns the scratch's bin counters to zero when it
+ * completes, so a scratch buffer that was zero-filled once (or passed to dirt_scratch_clear) and since
+ * used only by forwards with the same B, H, W, F and bin_capacity is "clean". */
+#define DIRT_FWD_SCRATCH_CLEAN 1u /* the scratch is clean: skip the forward's own clearing memset */
+/* zero_grad_vertices [B,V,4] / zero_grad_vertex_colors [B,V,C] (each may be NULL): accumulators the
+ * forward zero-fills in passing (inside its raster kernel), for a later dirt_rasterise_bwd with
+ * DIRT_BWD_ACCUMULATE -- a fixed-shape training loop then pays no separate clearing launch. */
 
 /* Backward: given grad_pixels = dL/dpixels, writes dL/dvertices [B,V,4] (z component is 0),
  * dL/dvertex_colors [B,V,C] and dL/dbackground [B,H,W,C].  All three outputs are fully
- * overwritten.  Filter-based (DIRT/OpenDR) derivative, DESIGN.md section 4. */
+ * overwritten (see DIRT_BWD_ACCUMULATE).  Filter-based (DIRT/OpenDR) derivative, DESIGN.md section 4. */
 int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces,
                        const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
                        const void *saved,
                        int B, int H, int W, int C, int V, int F,
                        float *grad_vertices, float *grad_vertex_colors, float *grad_background,
+                       unsigned flags, void *stream);
+/* flags of dirt_rasterise_bwd */
+#define DIRT_BWD_ACCUMULATE 1u /* add into grad_vertices / grad_vertex_colors instead of overwriting them
+                                  (e.g. zeroed by the caller on a side stream, off the critical path);
+                                  grad_background is always overwritten */
+/* Zero the bin counters of `scratch` for the next forward with the same B, H, W, F, bin_capacity
+ * (an async memset of a few KB; lets a caller clear them on another stream, see DIRT_FWD_SCRATCH_CLEAN). */
+int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *scratch, size_t scratch_bytes,
                        void *stream);
 
 /* Debug check (synchronises `stream`): returns DIRT_EFACE if any face index is outside [0,V). */

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_workspace_sizes():
     lib = _lib.load()
-    assert lib.dirt_abi_version() == 2
+    assert lib.dirt_abi_version() == 3
     saved, scratch = _lib.workspace_sizes(1, 1024, 1024, 3, 150000, 50000)
     assert saved >= 50000 * 6 * 128 + 50000 * 32  # 128-B records (6 slots/face) + 32-B face data
     assert scratch > 0
@@ -56,22 +56,30 @@ def test_invalid_arguments_raise_before_any_gpu_call(args, msg):
         _lib.workspace_sizes(*args)
     lib = _lib.load()
     B, H, W, C, V, F = args
-    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, B, H, W, C, V, F, 0, None, None, None, 0, None, 0, 0, None)
+    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, B, H, W, C, V, F, 0, None, None, None, 0, None, 0, 0, 0, None, None, None)
     assert rc == _lib.DIRT_EINVAL
     assert msg in lib.dirt_last_error().decode()
 
 
 def test_null_pointers_and_bad_shader_rejected():
     lib = _lib.load()
-    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, 1, 16, 16, 3, 3, 1, 0, None, None, None, 0, None, 0, 0, None)
+    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, 1, 16, 16, 3, 3, 1, 0, None, None, None, 0, None, 0, 0, 0, None, None, None)
     assert rc == _lib.DIRT_EINVAL and "null" in lib.dirt_last_error().decode()
-    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, 1, 16, 16, 3, 3, 1, 77, None, None, None, 0, None, 0, 0, None)
+    rc = lib.dirt_rasterise_fwd(None, None, None, None, None, 1, 16, 16, 3, 3, 1, 77, None, None, None, 0, None, 0, 0, 0, None, None, None)
     assert rc == _lib.DIRT_EINVAL and "shader" in lib.dirt_last_error().decode()
-    rc = lib.dirt_rasterise_bwd(None, None, None, None, None, None, None, 1, 16, 16, 3, 3, 1, None, None, None, None)
+    rc = lib.dirt_rasterise_bwd(None, None, None, None, None, None, None, 1, 16, 16, 3, 3, 1, None, None, None, 0, None)
     assert rc == _lib.DIRT_EINVAL
 
 
 def test_zero_batch_is_a_no_op():
     lib = _lib.load()
     assert lib.dirt_rasterise_fwd(None, None, None, None, None, 0, 16, 16, 3, 3, 1, 0, None, None, None, 0, None, 0, 0,
-                                  None) == _lib.DIRT_OK
+                                  0, None, None, None) == _lib.DIRT_OK
+
+
+def test_scratch_clear_validates_without_a_gpu():
+    lib = _lib.load()
+    # B == 0 is a no-op, a too-small scratch is rejected before any HIP call
+    assert lib.dirt_scratch_clear(0, 16, 16, 1, 0, None, 0, None) == _lib.DIRT_OK
+    assert lib.dirt_scratch_clear(1, 16, 16, 1, 0, None, 0, None) == _lib.DIRT_EINVAL
+    assert "scratch" in lib.dirt_last_error().decode()
