@@ -26,6 +26,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
+# measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc passes of this bench at c3;
+# produced by tools/gpu_traffic.sh + tools/pmc_traffic.py, committed with the round's profiles)
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 
 CONFIGS = {
     # name: (B per rank, H, W, C, F, radius_px)
@@ -165,8 +168,15 @@ def main():
     kbytes, fwd_b, bwd_b = alg_bytes(B, H, W, C, V, F)
     dom = max((k for k in kern_us if k in kbytes), key=lambda k: kern_us[k])
     achieved = kbytes[dom] / (kern_us[dom] * 1e-6) / 1e9
+    traffic = None
+    if args.config == "c3" and os.path.exists(TRAFFIC_JSON):
+        tk = json.load(open(TRAFFIC_JSON)).get("kernels", {})
+        hit = [v for k, v in tk.items() if k.split("<")[0] == dom]
+        if hit:
+            traffic = hit[0]["traffic_bytes"]
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic is not None else None,
                 "alg_bytes_per_launch": kbytes[dom], "avg_us": round(kern_us[dom], 2),
                 "op_frac": round((fwd_b + bwd_b) / (ms_per_step * 1e-3 / world) / 1e9 / HBM_PEAK_GBS, 4)}
 
