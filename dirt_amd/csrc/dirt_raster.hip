@@ -30,6 +30,8 @@
 
 #include "../../include/dirt_mi355x.h"
 #include "raster_rules.h"
+#include "oceanic.h"
+#include "oceanic.h"
 
 using namespace dirt;
 
@@ -614,7 +616,7 @@ __device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
 
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
-template <int CC, int AB = 0>
+template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
 __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      uint32_t *__restrict__ ccursor,
@@ -623,7 +625,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                                                      int B, int H, int W, int Cdyn, int V, int F, int ntx, int cshift,
                                                      int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
                                                      int32_t *__restrict__ gbuffer, float *__restrict__ zero_a,
-                                                     int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b)
+                                                     int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
+                                                     const float *__restrict__ verts, const float *__restrict__ cam)
 {
     if (!(AB & 16)) {
         // housekeeping spread over all blocks (a few KB each): return fill's bin cursors to zero for
@@ -793,9 +796,29 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     edge_values(r, i, j, E);
     float lam[3] = {0.0f, 0.0f, 0.0f};
     parent_lambda(r, E, lam);
-    const float *cb = colors + (int64_t)b * V * C;
-    const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
-    for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
+    if constexpr (SH == DIRT_SHADER_OCEANIC_HORIZON) {
+        // texCoordV = perspective-correct clip xy (shaders.cpp:19,21 alias texCoord to position); jitter by
+        // the background texel at (texCoordV+1)/2 (NEAREST), channels x,y (C=1 broadcast)
+        const float *vb = verts + (int64_t)b * V * 4;
+        const float *p0 = vb + (int64_t)fd.v[0] * 4, *p1 = vb + (int64_t)fd.v[1] * 4, *p2 = vb + (int64_t)fd.v[2] * 4;
+        const float tx = (lam[0] * p0[0] + lam[1] * p1[0]) + lam[2] * p2[0];
+        const float ty = (lam[0] * p0[1] + lam[1] * p1[1]) + lam[2] * p2[1];
+        const float u = (tx + 1.0f) / 2.0f, v = (ty + 1.0f) / 2.0f;
+        int ix = (int)floorf(u * (float)W), iy = (int)floorf(v * (float)H);
+        if (!(u * (float)W >= 0.0f)) ix = 0;
+        if (!(v * (float)H >= 0.0f)) iy = 0;
+        ix = ix < 0 ? 0 : (ix > W - 1 ? W - 1 : ix);
+        iy = iy < 0 ? 0 : (iy > H - 1 ? H - 1 : iy);
+        const float *texel = background + (((int64_t)b * H + (H - 1 - iy)) * W + ix) * C;
+        const float sx = texel[0], sy = C >= 2 ? texel[1] : texel[0];
+        const ocean::Camera camv{cam[0], cam[1], cam[2], cam[3], cam[4], cam[5], cam[6], cam[7]};
+        const float2 col = ocean::shade(tx + sx / (float)W, ty + sy / (float)H, camv, (float)W, (float)H);
+        for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 3 ? 1.0f : 0.0f;
+    } else {
+        const float *cb = colors + (int64_t)b * V * C;
+        const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
+        for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1498,10 +1521,12 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
                        size_t scratch_bytes, int64_t bin_capacity, unsigned flags, float *zero_grad_vertices,
                        float *zero_grad_vertex_colors, void *stream_)
 {
-    (void)camera_pos;
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
-    if (shader_id != DIRT_SHADER_GOURAUD) return fail(DIRT_EINVAL, "Rasterise: unsupported shader_id");
+    if (shader_id != DIRT_SHADER_GOURAUD && shader_id != DIRT_SHADER_OCEANIC_HORIZON)
+        return fail(DIRT_EINVAL, "Rasterise: unsupported shader_id");
+    if (shader_id == DIRT_SHADER_OCEANIC_HORIZON && !camera_pos)
+        return fail(DIRT_EINVAL, "Rasterise: the oceanic_horizon program needs camera_pos (8 floats)");
     if (B == 0) return DIRT_OK;
     if (!background || !pixels || !gbuffer || !saved || !scratch || (F > 0 && (!faces || !vertices)) ||
         (V > 0 && (!vertices || !vertex_colors)))
@@ -1547,12 +1572,20 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
 #define LAUNCH_RASTER(CC)                                                                                        \
+    if (shader_id == DIRT_SHADER_OCEANIC_HORIZON)                                                                \
+        raster_kernel<CC, 0, DIRT_SHADER_OCEANIC_HORIZON><<<grid, dim3(256), 0, stream>>>(                       \
+            background, vertex_colors, recs, fdata, ccursor, coffset, bins, L.bin_capacity, B, H, W, C, V, F,      \
+            L.ntx, L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices,                       \
+            zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos);                               \
+    else                                                                                                         \
     raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,   \
                                                       bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift,    \
                                                       L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices, \
                                                       zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
                                                       zero_grad_vertex_colors,                                     \
-                                                      zero_grad_vertex_colors ? (int64_t)B * V * C : 0)
+                                                      zero_grad_vertex_colors ? (int64_t)B * V * C : 0,            \
+                                                      vertices, camera_pos)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else LAUNCH_RASTER(0);
@@ -1631,7 +1664,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
         raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,\
                                                              bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift, \
                                                              L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, 0,  \
-                                                             nullptr, 0);                                           \
+                                                             nullptr, 0, nullptr, nullptr);                         \
         break
     switch (variant) {
         V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8);

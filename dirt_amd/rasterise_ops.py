@@ -119,14 +119,28 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
         camera_pos = _as_tensor(camera_pos, torch.float32, dev).contiguous().reshape(-1)
         if camera_pos.numel() < 8:
             raise ValueError("camera_pos must hold at least 8 floats (csrc/rasterise_egl.cpp:323)")
+    elif shader_id == _lib.SHADER_OCEANIC_HORIZON:
+        raise ValueError("the oceanic_horizon fragment program needs camera_pos (8 floats)")
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
     pixels, gbuffer = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos,
                                                int(height), int(width), int(channels), shader_id, int(bin_capacity))
     return (pixels, gbuffer) if return_gbuffer else pixels
 
 
+_SHADERS = {None: _lib.SHADER_GOURAUD, "gouraud": _lib.SHADER_GOURAUD,
+            "oceanic_horizon": _lib.SHADER_OCEANIC_HORIZON}
+
+
+def _shader_id(shader):
+    if isinstance(shader, int) and shader in _SHADERS.values():
+        return shader
+    if shader not in _SHADERS:
+        raise ValueError("unknown fragment program %r (expected 'gouraud' or 'oceanic_horizon')" % (shader,))
+    return _SHADERS[shader]
+
+
 def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None, channels=None,
-              name=None):
+              name=None, shader=None):
     """Rasterises the given `vertices` and `faces` over `background` (reference dirt/rasterise_ops.py:10-54).
 
     Args:
@@ -134,9 +148,15 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
         vertices: float32 [vertex count, 4] OpenGL clip-space positions
         vertex_colors: float32 [vertex count, channels]; interpolated perspective-correctly (Gouraud)
         faces: int32 [face count, 3] indices into `vertices`
-        camera_pos: optional float32 [>=8]; only read by procedural fragment programs
+        camera_pos: float32 [>=8] (cam x, y, z, ang1, ang2, ang3, time, light_z,
+            csrc/rasterise_egl.cpp:399-406); read only by the `oceanic_horizon` program
         height, width, channels: may be None, then inferred from `background`'s shape
         name: ignored (TensorFlow name scope in the reference)
+        shader: fragment program. None / 'gouraud': Gouraud colours (upstream DIRT, the default);
+            'oceanic_horizon': the program the fork's `Rasterise` op binds (csrc/shaders.cpp:1668-1919,
+            rasterise_egl.cpp:385): covered pixels get (sky mask, sun / reflection, 0), jittered by the
+            background's first two channels; needs camera_pos and has no gradient (the reference
+            registers none)
 
     Returns:
         float32 [height, width, channels] pixels, differentiable w.r.t. background, vertices, vertex_colors.
@@ -155,11 +175,11 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
     vertex_colors = _as_tensor(vertex_colors, torch.float32, dev)
     faces = _as_tensor(faces, torch.int32, dev)
     return _rasterise_batched(background[None], vertices[None], vertex_colors[None], faces[None], camera_pos,
-                              height, width, channels, _lib.SHADER_GOURAUD)[0]
+                              height, width, channels, _shader_id(shader))[0]
 
 
 def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
-                    channels=None, name=None):
+                    channels=None, name=None, shader=None):
     """Rasterises a batch of meshes with equal vertex and face counts (reference dirt/rasterise_ops.py:57-88).
 
     Conceptually `torch.stack([rasterise(bg_i, v_i, c_i, f_i) for ...])`; every argument carries a leading
@@ -174,7 +194,7 @@ def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None,
     if channels is None:
         channels = int(bshape[3])
     return _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels,
-                              _lib.SHADER_GOURAUD)
+                              _shader_id(shader))
 
 
 def _procedural(opname):

@@ -275,9 +275,198 @@ static int setup_frame(const float *verts, const int32_t *faces, int V, int F, i
 
 /* Forward: pixels [B,H,W,C] (rows top-first), gbuffer [B,H,W] record index or -1.
  * Returns 0, or 2 if a face index was out of range (such faces are culled). */
+/* ------------------------------------------------------------------------------------------------ */
+/* Fragment program 1: the fork's `oceanic_horizon` (csrc/shaders.cpp:1668-1919), restated in float32
+ * with the operation order of the GLSL source and no contraction.  GLSL's sin/cos/pow are the driver's
+ * (NVIDIA, unpinned); here they are fixed algorithms (OCEANIC.md-style spec in DESIGN.md §3b), written
+ * identically in the HIP path, so oracle and GPU agree bit for bit.
+ *   - sin/cos: 3-part Cody-Waite reduction by pi/2 (11+11+24-bit constants), cephes minimax polynomials;
+ *   - pow(x,y), x in [0,1]: exp2(y*log2(x)); log2 via atanh series on m in [sqrt(1/2), sqrt(2)),
+ *     exp2 via degree-6 polynomial, results below 2^-125 flush to 0 (as fp32 GLSL on the reference GPU);
+ *   - normalize(v) = v / sqrt(dot(v,v)) (IEEE sqrt and division), dot = (x*x' + y*y') + z*z'.
+ * The water() terms multiplied by small_waveheight = 0.0 (shaders.cpp:1690,1776-1785) are exact zeros
+ * (finite * 0) and are omitted. */
+
+static float ocn_sincos(float x, int want_cos)
+{
+    if (!(fabsf(x) < 1.0e30f)) return x - x; /* NaN for inf / NaN */
+    const float k = rintf(x * 0.636619772f);
+    float r = x - k * 1.5703125f;
+    r = r - k * 4.837512969970703125e-4f;
+    r = r - k * 7.549790126404332e-8f;
+    float q = k - 4.0f * floorf(k * 0.25f); /* quadrant 0..3 (exact while |k| < 2^24) */
+    if (want_cos) q = q + 1.0f;
+    if (q >= 4.0f) q = q - 4.0f;
+    const float z = r * r;
+    const float s = r + (r * z) * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+    const float c = (1.0f - 0.5f * z) +
+                    (z * z) * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
+    if (q == 0.0f) return s;
+    if (q == 1.0f) return c;
+    if (q == 2.0f) return -s;
+    return -c;
+}
+static float ocn_sin(float x) { return ocn_sincos(x, 0); }
+static float ocn_cos(float x) { return ocn_sincos(x, 1); }
+
+static float ocn_bits_to_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static uint32_t ocn_f_to_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+/* log2(x) for normal x > 0 */
+static float ocn_log2(float x)
+{
+    const uint32_t u = ocn_f_to_bits(x);
+    float e = (float)((int)((u >> 23) & 0xffu) - 126);
+    float m = ocn_bits_to_f((u & 0x807fffffu) | 0x3f000000u); /* [0.5, 1) */
+    if (m < 0.70710678f) {
+        m = m * 2.0f;
+        e = e - 1.0f;
+    }
+    const float t = (m - 1.0f) / (m + 1.0f);
+    const float t2 = t * t;
+    const float l = t * (2.885390082f + t2 * (0.9617966939f + t2 * (0.5770780164f + t2 * (0.4121985831f +
+                                                                                         t2 * 0.3205988980f))));
+    return e + l;
+}
+
+/* 2^z for z <= 0 (pow of [0,1] by a positive exponent) */
+static float ocn_exp2(float z)
+{
+    if (!(z >= -125.0f)) return 0.0f; /* also NaN -> 0 */
+    const float n = floorf(z + 0.5f);
+    const float f = z - n; /* [-0.5, 0.5] */
+    const float p = 1.0f + f * (0.6931471806f + f * (0.2402265070f + f * (0.05550410866f + f * (0.009618129108f +
+                    f * (0.001333355815f + f * 0.0001540353039f)))));
+    return ldexpf(p, (int)n);
+}
+
+/* GLSL pow(x, y) for x = clamp(...) in [0,1], y > 0 */
+static float ocn_pow01(float x, float y)
+{
+    if (!(x >= 1.17549435e-38f)) return 0.0f; /* 0, denormal (flushed) or NaN */
+    if (x >= 1.0f) return 1.0f;
+    return ocn_exp2(y * ocn_log2(x));
+}
+
+static float ocn_clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+static float ocn_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+static float ocn_dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+static void ocn_normalize(float v[3])
+{
+    const float l = sqrtf(ocn_dot3(v, v));
+    v[0] = v[0] / l; v[1] = v[1] / l; v[2] = v[2] / l;
+}
+
+/* water(p), shaders.cpp:1760-1791 with small_waveheight = 0 */
+static float ocn_water(float px, float py, float time)
+{
+    float height = 70.0f;
+    const float shift2x = 0.001f * ((time * 190.0f) * 2.0f);
+    float wave = 0.0f;
+    wave = wave + ocn_sin(px * 0.021f + shift2x) * 4.5f;
+    wave = wave + ocn_sin((px * 0.0172f + py * 0.010f) + shift2x * 1.121f) * 4.0f;
+    wave = wave - ocn_sin((px * 0.00104f + py * 0.005f) + shift2x * 0.121f) * 4.0f;
+    wave = wave + ocn_sin((px * 0.02221f + py * 0.01233f) + shift2x * 3.437f) * 5.0f;
+    wave = wave + ocn_sin((px * 0.03112f + py * 0.01122f) + shift2x * 4.269f) * 2.5f;
+    wave = wave * 1.0f; /* large_waveheight */
+    height = height + wave;
+    return height;
+}
+
+/* trace(), shaders.cpp:1817-1856 (RENDER_GODRAYS undefined -> fog stays 0) */
+static int ocn_trace(const float ro[3], const float rd[3], float time, float *dist)
+{
+    float t = -ro[1] / rd[1];
+    float st = 0.5f;
+    float old_h = 0.0f;
+    for (int j = 1000; j < 1020; ++j) {
+        if (t > 500.0f) st = 1.0f;
+        if (t > 800.0f) st = 2.0f;
+        if (t > 1500.0f) st = 3.0f;
+        const float p0 = ro[0] + t * rd[0], p1 = ro[1] + t * rd[1], p2 = ro[2] + t * rd[2];
+        const float h = p1 - ocn_water(p0, p2, time);
+        t = t + (fmaxf(1.0f, fabsf(h)) * ocn_sign(h)) * st;
+        if (old_h * h < 0.0f) st = st / 2.0f;
+        old_h = h;
+    }
+    *dist = t;
+    return !(rd[1] > 0.0f);
+}
+
+/* main(), shaders.cpp:1858-1917: xy = texCoordV + jitter; writes (col.x, col.y) */
+static void ocn_shade(float xyx, float xyy, const float *cam, float width, float height, float out[2])
+{
+    const float ro[3] = {cam[0], cam[1], cam[2]};
+    const float time = cam[6];
+    float light[3] = {0.1f, 0.25f, cam[7]};
+    ocn_normalize(light);
+    float rdv[3];
+    rdv[0] = (xyx + 1.0f) * width / 2.0f - width / 2.0f;
+    rdv[1] = (xyy + 1.0f) * height / 2.0f - height / 2.0f;
+    rdv[2] = 1.73f * width / 2.0f;
+    ocn_normalize(rdv);
+    const float sin1 = ocn_sin(cam[3]), cos1 = ocn_cos(cam[3]);
+    const float sin2 = ocn_sin(cam[4]), cos2 = ocn_cos(cam[4]);
+    const float sin3 = ocn_sin(cam[5]), cos3 = ocn_cos(cam[5]);
+    float rd[3];
+    rd[0] = ((cos2 * cos3) * rdv[0] + (-cos1 * sin3 + (sin1 * sin2) * cos3) * rdv[1]) +
+            (sin1 * sin3 + (cos1 * sin2) * cos3) * rdv[2];
+    rd[1] = ((cos2 * sin3) * rdv[0] + (cos1 * cos3 + (sin1 * sin2) * sin3) * rdv[1]) +
+            (-sin1 * cos3 + (cos1 * sin2) * sin3) * rdv[2];
+    rd[2] = (-sin2 * rdv[0] + (sin1 * cos2) * rdv[1]) + (cos1 * cos2) * rdv[2];
+    float sundot = ocn_clamp01(ocn_dot3(rd, light));
+    float dist = 0.0f;
+    if (!ocn_trace(ro, rd, time, &dist)) {
+        out[0] = 1.0f;
+        out[1] = ocn_pow01(sundot, 350.0f);
+        return;
+    }
+    out[0] = 0.0f;
+    const float wx = ro[0] + dist * rd[0], wz = ro[2] + dist * rd[2];
+    const float d = 0.1f * 1.0f * 4.0f; /* 0.1 * wavegain * 4 */
+    float n[3] = {ocn_water(wx - d, wz, time) - ocn_water(wx + d, wz, time), 1.0f,
+                  ocn_water(wx, wz - d, time) - ocn_water(wx, wz + d, time)};
+    ocn_normalize(n);
+    const float dn = 2.0f * ocn_dot3(n, rd); /* reflect(I, N) = I - 2 dot(N, I) N */
+    const float rr[3] = {rd[0] - dn * n[0], rd[1] - dn * n[1], rd[2] - dn * n[2]};
+    sundot = ocn_clamp01(ocn_dot3(rr, light));
+    out[1] = (0.5f * ocn_pow01(sundot, 10.0f) + 0.25f * ocn_pow01(sundot, 3.5f)) + 0.75f * ocn_pow01(sundot, 300.0f);
+}
+
+/* texCoordV = perspective-correct interpolation of the vertices' clip xy (shaders.cpp:19,21 alias
+ * texCoord to position); jitter = background texel at (texCoordV+1)/2 (NEAREST; at texel centres the
+ * reference's LINEAR magnification returns the same texel), channels x,y (C=1 broadcast,
+ * rasterise_egl.cu:39-47) divided by (width, height) (shaders.cpp:1865-1867) */
+void oracle_oceanic_horizon_pixel(const float *bgframe, int H, int W, int C, float tx, float ty, const float *cam,
+                                  float out[2])
+{
+    const float u = (tx + 1.0f) / 2.0f, v = (ty + 1.0f) / 2.0f;
+    int ix = (int)floorf(u * (float)W), iy = (int)floorf(v * (float)H);
+    if (!(u * (float)W >= 0.0f)) ix = 0;
+    if (!(v * (float)H >= 0.0f)) iy = 0;
+    ix = ix < 0 ? 0 : (ix > W - 1 ? W - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > H - 1 ? H - 1 : iy);
+    const float *texel = bgframe + (((int64_t)(H - 1 - iy)) * W + ix) * C;
+    const float sx = texel[0], sy = C >= 2 ? texel[1] : texel[0];
+    ocn_shade(tx + sx / (float)W, ty + sy / (float)H, cam, (float)W, (float)H, out);
+}
+
+int oracle_rasterise_fwd_shader(const float *background, const float *vertices, const float *vertex_colors,
+                                const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
+                                const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads);
+
 int oracle_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
                          const int32_t *faces, int B, int H, int W, int C, int V, int F,
                          float *pixels, int32_t *gbuffer, int nthreads)
+{
+    return oracle_rasterise_fwd_shader(background, vertices, vertex_colors, faces, B, H, W, C, V, F, 0, NULL,
+                                       pixels, gbuffer, nthreads);
+}
+
+/* shader_id 0 = Gouraud, 1 = oceanic_horizon (camera_pos: 8 host floats, rasterise_egl.cpp:399-406) */
+int oracle_rasterise_fwd_shader(const float *background, const float *vertices, const float *vertex_colors,
+                                const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
+                                const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
 {
     int status = 0;
 #ifdef _OPENMP
@@ -338,6 +527,18 @@ int oracle_rasterise_fwd(const float *background, const float *vertices, const f
                     float lam[3] = {0.0f, 0.0f, 0.0f};
                     parent_lambda(r, E, lam);
                     const int32_t *f3 = fb + 3 * (int64_t)r->face;
+                    if (shader_id == 1) {
+                        /* fragColor = (col.x, col.y, 0, 1) (shaders.cpp:1860-1862,1916) */
+                        const float tx = (lam[0] * vb[(int64_t)f3[0] * 4] + lam[1] * vb[(int64_t)f3[1] * 4]) +
+                                         lam[2] * vb[(int64_t)f3[2] * 4];
+                        const float ty = (lam[0] * vb[(int64_t)f3[0] * 4 + 1] + lam[1] * vb[(int64_t)f3[1] * 4 + 1]) +
+                                         lam[2] * vb[(int64_t)f3[2] * 4 + 1];
+                        float col[2];
+                        oracle_oceanic_horizon_pixel(background + (int64_t)b * H * W * C, H, W, C, tx, ty,
+                                                     camera_pos, col);
+                        for (int c = 0; c < C; ++c) out[c] = c == 0 ? col[0] : c == 1 ? col[1] : c == 3 ? 1.0f : 0.0f;
+                        continue;
+                    }
                     for (int c = 0; c < C; ++c)
                         out[c] = (lam[0] * cb[(int64_t)f3[0] * C + c] + lam[1] * cb[(int64_t)f3[1] * C + c]) +
                                  lam[2] * cb[(int64_t)f3[2] * C + c];

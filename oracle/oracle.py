@@ -28,6 +28,10 @@ def load():
         P, I = ctypes.c_void_p, ctypes.c_int
         lib.oracle_rasterise_fwd.argtypes = [P, P, P, P, I, I, I, I, I, I, P, P, I]
         lib.oracle_rasterise_fwd.restype = I
+        lib.oracle_rasterise_fwd_shader.argtypes = [P, P, P, P, I, I, I, I, I, I, I, P, P, P, I]
+        lib.oracle_rasterise_fwd_shader.restype = I
+        lib.oracle_oceanic_horizon_pixel.argtypes = [P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
+        lib.oracle_oceanic_horizon_pixel.restype = None
         lib.oracle_rasterise_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, I]
         lib.oracle_rasterise_bwd.restype = I
         lib.oracle_max_threads.argtypes = []
@@ -48,8 +52,9 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0):
+def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0, shader_id=0, camera_pos=None):
     """Batched forward.  background [B,H,W,C], vertices [B,V,4], vertex_colors [B,V,C], faces [B,F,3].
+    shader_id 0 = Gouraud, 1 = oceanic_horizon (camera_pos: 8 floats).
 
     Returns (pixels [B,H,W,C] float32, gbuffer [B,H,W] int32 record index or -1, status)."""
     bg, vs, cs, fs = _f32(background), _f32(vertices), _f32(vertex_colors), _i32(faces)
@@ -57,9 +62,22 @@ def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0):
     V, F = vs.shape[1], fs.shape[1]
     pixels = np.empty((B, H, W, C), np.float32)
     gbuf = np.empty((B, H, W), np.int32)
-    st = load().oracle_rasterise_fwd(_ptr(bg), _ptr(vs), _ptr(cs), _ptr(fs), B, H, W, C, V, F,
-                                     _ptr(pixels), _ptr(gbuf), nthreads)
+    cam = _f32(camera_pos if camera_pos is not None else np.zeros(8))
+    if shader_id == 1 and cam.size < 8:
+        raise ValueError("oceanic_horizon needs camera_pos with at least 8 floats")
+    st = load().oracle_rasterise_fwd_shader(_ptr(bg), _ptr(vs), _ptr(cs), _ptr(fs), B, H, W, C, V, F, shader_id,
+                                            _ptr(cam), _ptr(pixels), _ptr(gbuf), nthreads)
     return pixels, gbuf, st
+
+
+def oceanic_horizon_pixel(background_frame, tx, ty, camera_pos):
+    """The fragment program alone at texCoordV = (tx, ty) of a [H,W,C] background: returns (col.x, col.y)."""
+    bg = _f32(background_frame)
+    H, W, C = bg.shape
+    out = np.zeros(2, np.float32)
+    cam = _f32(camera_pos)
+    load().oracle_oceanic_horizon_pixel(_ptr(bg), H, W, C, float(tx), float(ty), _ptr(cam), _ptr(out))
+    return out
 
 
 def rasterise_bwd(vertices, vertex_colors, faces, pixels, grad_pixels, gbuffer, nthreads=0):

@@ -14,13 +14,17 @@ def test_op_names_and_signatures_match_the_reference():
     # dirt/rasterise_ops.py:10,57,91,110,129,148,167,186 (camera_pos made optional)
     for name in ("rasterise", "rasterise_batch"):
         params = list(inspect.signature(getattr(dirt_amd, name)).parameters)
+        # the reference's parameters in its order; `shader` is an added keyword (fork's fragment program)
         assert params == ["background", "vertices", "vertex_colors", "faces", "camera_pos", "height", "width",
-                          "channels", "name"]
+                          "channels", "name", "shader"]
         sig = inspect.signature(getattr(dirt_amd, name))
         assert all(sig.parameters[p].default is None for p in params[4:])
     for name in ("rasterise_grad", "oceanic_no_cloud", "oceanic_simple_proxy", "oceanic_still_cloud",
                  "oceanic_opt_flow", "hill"):
         assert callable(getattr(dirt_amd, name))
+    with pytest.raises(ValueError, match="fragment program"):
+        rasterise_ops._shader_id("phong")
+    assert rasterise_ops._shader_id("oceanic_horizon") == 1 and rasterise_ops._shader_id(None) == 0
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")

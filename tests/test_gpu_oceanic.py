@@ -1,0 +1,78 @@
+"""GPU parity of the `oceanic_horizon` fragment program (shader_id 1): the HIP resolve
+against the CPU oracle, bit for bit (both state the GLSL of csrc/shaders.cpp:1668-1919 in float32 with
+the same fixed sin/cos/pow algorithms, no contraction, IEEE division and sqrt)."""
+import numpy as np
+import pytest
+import torch
+
+import scenes
+from oracle import oracle
+from test_oceanic_oracle import CAMS, fullscreen
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_fwd(bg, v, c, f, cam):
+    from dirt_amd import rasterise_ops
+    t = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (bg, v, c, f)]
+    B, H, W, C = bg.shape
+    px, gb = rasterise_ops._rasterise_batched(*t, torch.tensor(cam, dtype=torch.float32).cuda(), H, W, C, 1,
+                                              return_gbuffer=True)
+    return px.cpu().numpy(), gb.cpu().numpy()
+
+
+def check(bg, v, c, f, cam):
+    px, gb = gpu_fwd(bg, v, c, f, cam)
+    rpx, rgb, _ = oracle.rasterise_fwd(bg, v, c, f, shader_id=1, camera_pos=np.array(cam, np.float32))
+    np.testing.assert_array_equal(gb, rgb)
+    np.testing.assert_array_equal(px, rpx)
+    return px
+
+
+@pytest.mark.parametrize("name", sorted(CAMS))
+def test_fullscreen_harness_960x640(name):
+    px = check(*fullscreen(640, 960), CAMS[name])
+    assert 0.0 < px[0, ..., 0].mean() < 1.0
+
+
+def test_background_jitter_and_channel_counts():
+    H, W = 96, 128
+    bg = np.random.default_rng(3).uniform(-3, 3, size=(H, W, 4)).astype(np.float32)
+    for C in (1, 3, 4):
+        check(*fullscreen(H, W, C=C, background=bg[..., :C].copy()), CAMS["square_test"])
+
+
+def test_mesh_with_perspective_and_uncovered_pixels():
+    bg, v, c, f = scenes.random_triangles(F=600, W=160, H=120, radius_px=20.0, seed=4, perspective=True)
+    check(bg[None], v[None], c[None], f[None], CAMS["rolled_moving"])
+    bg, v, c, f = scenes.batch_of(scenes.random_triangles, 3, F=300, W=96, H=64, radius_px=12.0, seed=9)
+    check(bg, v, c, f, CAMS["optimize_horizon"])
+
+
+def test_public_api_and_no_gradient():
+    import dirt_amd
+    bg, v, c, f = (a[0] for a in fullscreen(64, 96))
+    cam = torch.tensor(CAMS["optimize_horizon"]).cuda()
+    px = dirt_amd.rasterise(torch.from_numpy(bg).cuda(), torch.from_numpy(v).cuda().requires_grad_(True),
+                            torch.from_numpy(c).cuda(), torch.from_numpy(f).cuda(), camera_pos=cam,
+                            shader="oceanic_horizon")
+    ref, _, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None], shader_id=1,
+                                     camera_pos=np.array(CAMS["optimize_horizon"], np.float32))
+    np.testing.assert_array_equal(px.detach().cpu().numpy(), ref[0])
+    with pytest.raises(RuntimeError, match="gradient"):
+        px.sum().backward()
+    with pytest.raises(ValueError, match="camera_pos"):
+        dirt_amd.rasterise(torch.from_numpy(bg).cuda(), torch.from_numpy(v).cuda(), torch.from_numpy(c).cuda(),
+                           torch.from_numpy(f).cuda(), shader="oceanic_horizon")
+
+
+def test_session_oceanic_matches_op():
+    from dirt_amd.session import RasteriseSession
+    bg, v, c, f = fullscreen(128, 192)
+    cam = torch.tensor(CAMS["square_test"]).cuda()
+    sess = RasteriseSession(1, 128, 192, 3, 4, 2, shader_id=1)
+    t = [torch.from_numpy(a).cuda() for a in (bg, v, c, f)]
+    for _ in range(2):
+        px = sess.forward(*t, camera_pos=cam)
+    ref, _, _ = oracle.rasterise_fwd(bg, v, c, f, shader_id=1, camera_pos=np.array(CAMS["square_test"], np.float32))
+    np.testing.assert_array_equal(px.cpu().numpy(), ref)
