@@ -242,6 +242,63 @@ __device__ __forceinline__ void load_bbox(const Rec &r, uint32_t &bx, uint32_t &
     by = q.y;
 }
 
+// Records that span many coarse tiles (large triangles) would serialise one thread over all their
+// tiles; they are queued in LDS and their (record, coarse tile) pairs are spread over the whole
+// workgroup instead.  Small records (<= kSmallPairs tiles) stay with their thread.
+constexpr int kSmallPairs = 8;
+constexpr int kBigCap = 64;
+struct BigQueue {
+    int32_t ri[kBigCap];
+    uint32_t bx[kBigCap], by[kBigCap];
+    int32_t cx0[kBigCap], cy0[kBigCap], w[kBigCap], start[kBigCap + 1];
+    int32_t n;
+};
+
+// Call op(ri, bx, by, cx, cy) for every coarse tile of a record: inline when small or when the queue is
+// full, else queue it for coarse_pairs_flush.
+template <class Op>
+__device__ __forceinline__ void coarse_pairs_add(BigQueue &Q, int32_t ri, uint32_t bx, uint32_t by, int cshift, Op op)
+{
+    if ((bx & 0xffff) > (bx >> 16)) return;
+    int cx0, cx1, cy0, cy1;
+    coarse_range(bx, by, cshift, cx0, cx1, cy0, cy1);
+    const int w = cx1 - cx0 + 1, n = w * (cy1 - cy0 + 1);
+    if (n > kSmallPairs) {
+        const int q = atomicAdd(&Q.n, 1);
+        if (q < kBigCap) {
+            Q.ri[q] = ri; Q.bx[q] = bx; Q.by[q] = by; Q.cx0[q] = cx0; Q.cy0[q] = cy0; Q.w[q] = w;
+            Q.start[q + 1] = n;
+            return;
+        }
+    }
+    for (int cy = cy0; cy <= cy1; ++cy)
+        for (int cx = cx0; cx <= cx1; ++cx) op(ri, bx, by, cx, cy);
+}
+
+// Whole workgroup (converged): expand the queued records' pairs over all threads; resets the queue.
+template <int NT, class Op>
+__device__ __forceinline__ void coarse_pairs_flush(BigQueue &Q, Op op)
+{
+    __syncthreads();
+    const int nq = min(Q.n, kBigCap);
+    if (threadIdx.x == 0) {
+        Q.start[0] = 0;
+        for (int q = 0; q < nq; ++q) Q.start[q + 1] += Q.start[q];
+    }
+    __syncthreads();
+    const int total = Q.start[nq];
+    int q = 0;
+    for (int k = threadIdx.x; k < total; k += NT) {
+        while (Q.start[q + 1] <= k) ++q;  // k only grows: a forward walk over the (short) queue
+        const int local = k - Q.start[q];
+        const int cy = Q.cy0[q] + local / Q.w[q], cx = Q.cx0[q] + local % Q.w[q];
+        op(Q.ri[q], Q.bx[q], Q.by[q], cx, cy);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) Q.n = 0;
+    __syncthreads();
+}
+
 constexpr int kScanThreads = 1024;
 constexpr int kScanPerThread = 4;
 
@@ -311,9 +368,12 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
                                                             int64_t nc)
 {
     __shared__ uint32_t hist[kMaxCoarse];
+    __shared__ BigQueue Q;
     const int b = blockIdx.y, t = threadIdx.x;
     for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
+    if (t == 0) Q.n = 0;
     __syncthreads();
+    auto count = [&](int32_t, uint32_t, uint32_t, int cx, int cy) { atomicAdd(&hist[cy * nctx + cx], 1u); };
     Rec *frame_recs = recs + (int64_t)b * nrec;
     const float *vb = verts + (int64_t)b * V * 4;
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
@@ -357,11 +417,8 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
             make_record(tri.v, id, W, H, f, r);
             nsub = 1;
             frame_recs[f] = r;
-            if (r.i0 <= r.i1) {
-                const int cx0 = r.i0 >> cshift, cx1 = r.i1 >> cshift, cy0 = r.j0 >> cshift, cy1 = r.j1 >> cshift;
-                for (int cy = cy0; cy <= cy1; ++cy)
-                    for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&hist[cy * nctx + cx], 1u);
-            }
+            coarse_pairs_add(Q, f, (uint32_t)r.i0 | ((uint32_t)r.i1 << 16), (uint32_t)r.j0 | ((uint32_t)r.j1 << 16),
+                             cshift, count);
         } else {
             frame_recs[f] = r;  // empty unless clip_face overwrites it
 #ifndef DIRT_SETUP_NO_CLIP
@@ -372,18 +429,15 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
 #endif
             for (int s = 0; s < nsub; ++s) {
                 uint32_t bx, by;
-                load_bbox(frame_recs[rec_index(F, f, s)], bx, by);
-                if ((bx & 0xffff) > (bx >> 16)) continue;
-                int cx0, cx1, cy0, cy1;
-                coarse_range(bx, by, cshift, cx0, cx1, cy0, cy1);
-                for (int cy = cy0; cy <= cy1; ++cy)
-                    for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&hist[cy * nctx + cx], 1u);
+                const int64_t ri = rec_index(F, f, s);
+                load_bbox(frame_recs[ri], bx, by);
+                coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, count);
             }
         }
         fd.nsub = nsub;
         fdata[gid] = fd;
     }
-    __syncthreads();
+    coarse_pairs_flush<kBinThreads>(Q, count);
     uint32_t *cc = ccount + (int64_t)b * ncoarse;
     // count atomics WITH return: a returned value means the add has been performed at the coherence
     // point, so after the barrier this block's counts are all in before its ticket (no release fence,
@@ -421,31 +475,6 @@ __device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, i
     return (uint32_t)a0 | ((uint32_t)a1 << 8) | ((uint32_t)b0 << 16) | ((uint32_t)b1 << 24);
 }
 
-template <bool kPass2>
-__device__ __forceinline__ void bin_face_records(const Rec *__restrict__ frame_recs, int F, int f, int nsub, int cshift,
-                                                 int nctx, uint32_t *hist, const uint64_t *base,
-                                                 uint2 *__restrict__ bins, int64_t capacity)
-{
-    for (int s = 0; s < nsub; ++s) {
-        const int64_t ri = rec_index(F, f, s);
-        uint32_t bx, by;
-        load_bbox(frame_recs[ri], bx, by);
-        if ((bx & 0xffff) > (bx >> 16)) continue;
-        int cx0, cx1, cy0, cy1;
-        coarse_range(bx, by, cshift, cx0, cx1, cy0, cy1);
-        for (int cy = cy0; cy <= cy1; ++cy)
-            for (int cx = cx0; cx <= cx1; ++cx) {
-                const int c = cy * nctx + cx;
-                if (!kPass2) {
-                    atomicAdd(&hist[c], 1u);
-                } else {
-                    const uint64_t dst = base[c] + atomicAdd(&hist[c], 1u);
-                    if (dst < (uint64_t)capacity) bins[dst] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
-                }
-            }
-    }
-}
-
 __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict__ recs,
                                                            const FaceData *__restrict__ fdata, int F, int cshift,
                                                            int nctx, int ncoarse, int64_t nrec,
@@ -456,6 +485,7 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
 {
     __shared__ uint32_t hist[kMaxCoarse];
     __shared__ uint64_t base[kMaxCoarse];
+    __shared__ BigQueue Q;
     const int b = blockIdx.y, t = threadIdx.x;
     {
         // self-cleaning scratch: nothing reads the counts after setup's scan (the raster uses offset
@@ -467,14 +497,27 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
     for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
     __syncthreads();
     const Rec *frame_recs = recs + (int64_t)b * nrec;
+    if (t == 0) Q.n = 0;
     int nsub[kFacesPerThread];
+    auto count = [&](int32_t, uint32_t, uint32_t, int cx, int cy) { atomicAdd(&hist[cy * nctx + cx], 1u); };
+    auto place = [&](int32_t ri, uint32_t bx, uint32_t by, int cx, int cy) {
+        const int c = cy * nctx + cx;
+        const uint64_t dst = base[c] + atomicAdd(&hist[c], 1u);
+        if (dst < (uint64_t)capacity) bins[dst] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
+    };
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < kFacesPerThread; ++q) {
         const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
         nsub[q] = f < F ? fdata[(int64_t)b * F + f].nsub : 0;
-        bin_face_records<false>(frame_recs, F, f, nsub[q], cshift, nctx, hist, nullptr, bins, capacity);
+        for (int s = 0; s < nsub[q]; ++s) {
+            const int64_t ri = rec_index(F, f, s);
+            uint32_t bx, by;
+            load_bbox(frame_recs[ri], bx, by);
+            coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, count);
+        }
     }
-    __syncthreads();
+    coarse_pairs_flush<kBinThreads>(Q, count);
     const int64_t cb = (int64_t)b * ncoarse;
     for (int c = t; c < ncoarse; c += kBinThreads) {
         const uint32_t n = hist[c];
@@ -485,8 +528,14 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
 #pragma unroll
     for (int q = 0; q < kFacesPerThread; ++q) {
         const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
-        bin_face_records<true>(frame_recs, F, f, nsub[q], cshift, nctx, hist, base, bins, capacity);
+        for (int s = 0; s < nsub[q]; ++s) {
+            const int64_t ri = rec_index(F, f, s);
+            uint32_t bx, by;
+            load_bbox(frame_recs[ri], bx, by);
+            coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, place);
+        }
     }
+    coarse_pairs_flush<kBinThreads>(Q, place);
 }
 
 // ------------------------------------------------------------------------------------------------
