@@ -698,7 +698,10 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const int C = CC > 0 ? CC : Cdyn;
     __shared__ int32_t s_list_all[kStrips][kListCap];
     __shared__ StripEntry s_ent_all[kStrips][64];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
+    // Gouraud: XCD bands (L2 sharing of bins / records between neighbouring tiles); a procedural
+    // program is compute-bound and its cost follows the image content (sky vs water), so its tiles are
+    // interleaved over the XCDs instead (round-robin dispatch order) for balance
+    const int tile = SH == DIRT_SHADER_GOURAUD ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
     const int t = threadIdx.x, lx = t & 15, ly = t >> 4, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);

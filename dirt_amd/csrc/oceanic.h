@@ -27,6 +27,25 @@ __device__ __forceinline__ float sincos_fixed(float x, bool want_cos)
     return q == 0.0f ? s : q == 1.0f ? c : q == 2.0f ? -s : -c;
 }
 __device__ __forceinline__ float sin_fixed(float x) { return sincos_fixed(x, false); }
+
+// sin for water() (the hot loop): one reduction by pi, odd Taylor polynomial to x^11 on [-pi/2, pi/2],
+// sign by the parity of k (the oracle's ocn_sin_pi)
+__device__ __forceinline__ float sin_pi_fixed(float x)
+{
+    if (!(fabsf(x) < 1.0e30f)) return x - x;
+    const float k = __builtin_rintf(x * 0.318309873f);
+    float r = fmaf(-k, 3.140625f, x);  // explicit fused multiply-adds, as the oracle's fmaf
+    r = fmaf(-k, 9.675025939941406e-4f, r);
+    r = fmaf(-k, 1.5099580252808664e-7f, r);
+    const float z = r * r;
+    float p = fmaf(z, -2.5052107943679403e-8f, 2.7557318844628753e-6f);
+    p = fmaf(z, p, -1.9841270113829523e-4f);
+    p = fmaf(z, p, 8.333333767950535e-3f);
+    p = fmaf(z, p, -1.666666716337204e-1f);
+    const float sn = fmaf(r * z, p, r);
+    const float parity = k - 2.0f * floorf(k * 0.5f);
+    return parity == 1.0f ? -sn : sn;
+}
 __device__ __forceinline__ float cos_fixed(float x) { return sincos_fixed(x, true); }
 
 __device__ __forceinline__ float log2_fixed(float x)  // normal x > 0
@@ -73,11 +92,11 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
 __device__ __forceinline__ float water(float px, float py, float shift2x)
 {
     float wave = 0.0f;
-    wave = wave + sin_fixed(px * 0.021f + shift2x) * 4.5f;
-    wave = wave + sin_fixed((px * 0.0172f + py * 0.010f) + shift2x * 1.121f) * 4.0f;
-    wave = wave - sin_fixed((px * 0.00104f + py * 0.005f) + shift2x * 0.121f) * 4.0f;
-    wave = wave + sin_fixed((px * 0.02221f + py * 0.01233f) + shift2x * 3.437f) * 5.0f;
-    wave = wave + sin_fixed((px * 0.03112f + py * 0.01122f) + shift2x * 4.269f) * 2.5f;
+    wave = wave + sin_pi_fixed(px * 0.021f + shift2x) * 4.5f;
+    wave = wave + sin_pi_fixed((px * 0.0172f + py * 0.010f) + shift2x * 1.121f) * 4.0f;
+    wave = wave - sin_pi_fixed((px * 0.00104f + py * 0.005f) + shift2x * 0.121f) * 4.0f;
+    wave = wave + sin_pi_fixed((px * 0.02221f + py * 0.01233f) + shift2x * 3.437f) * 5.0f;
+    wave = wave + sin_pi_fixed((px * 0.03112f + py * 0.01122f) + shift2x * 4.269f) * 2.5f;
     wave = wave * 1.0f;  // large_waveheight
     return 70.0f + wave;
 }

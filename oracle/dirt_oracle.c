@@ -284,6 +284,8 @@ static int setup_frame(const float *verts, const int32_t *faces, int V, int F, i
  *   - pow(x,y), x in [0,1]: exp2(y*log2(x)); log2 via atanh series on m in [sqrt(1/2), sqrt(2)),
  *     exp2 via degree-6 polynomial, results below 2^-125 flush to 0 (as fp32 GLSL on the reference GPU);
  *   - normalize(v) = v / sqrt(dot(v,v)) (IEEE sqrt and division), dot = (x*x' + y*y') + z*z'.
+ *   - water()'s sines: one reduction by pi and an odd degree-11 polynomial, written with explicit fmaf
+ *     (correctly rounded on both sides, so still bit-identical) (ocn_sin_pi);
  * The water() terms multiplied by small_waveheight = 0.0 (shaders.cpp:1690,1776-1785) are exact zeros
  * (finite * 0) and are omitted. */
 
@@ -307,6 +309,25 @@ static float ocn_sincos(float x, int want_cos)
     return -c;
 }
 static float ocn_sin(float x) { return ocn_sincos(x, 0); }
+
+/* sin for water(): one reduction by pi (3.140625 + 9.675025939941406e-4 + 1.509958025e-7) and the odd
+ * Taylor polynomial to x^11 on [-pi/2, pi/2] (1.5e-7 absolute error for |x| < 3000), sign by parity */
+static float ocn_sin_pi(float x)
+{
+    if (!(fabsf(x) < 1.0e30f)) return x - x;
+    const float k = rintf(x * 0.318309873f);
+    float r = fmaf(-k, 3.140625f, x); /* explicit fused multiply-adds (correctly rounded in C and on the GPU) */
+    r = fmaf(-k, 9.675025939941406e-4f, r);
+    r = fmaf(-k, 1.5099580252808664e-7f, r);
+    const float z = r * r;
+    float p = fmaf(z, -2.5052107943679403e-8f, 2.7557318844628753e-6f);
+    p = fmaf(z, p, -1.9841270113829523e-4f);
+    p = fmaf(z, p, 8.333333767950535e-3f);
+    p = fmaf(z, p, -1.666666716337204e-1f);
+    const float sn = fmaf(r * z, p, r);
+    const float parity = k - 2.0f * floorf(k * 0.5f);
+    return parity == 1.0f ? -sn : sn;
+}
 static float ocn_cos(float x) { return ocn_sincos(x, 1); }
 
 static float ocn_bits_to_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
@@ -363,11 +384,11 @@ static float ocn_water(float px, float py, float time)
     float height = 70.0f;
     const float shift2x = 0.001f * ((time * 190.0f) * 2.0f);
     float wave = 0.0f;
-    wave = wave + ocn_sin(px * 0.021f + shift2x) * 4.5f;
-    wave = wave + ocn_sin((px * 0.0172f + py * 0.010f) + shift2x * 1.121f) * 4.0f;
-    wave = wave - ocn_sin((px * 0.00104f + py * 0.005f) + shift2x * 0.121f) * 4.0f;
-    wave = wave + ocn_sin((px * 0.02221f + py * 0.01233f) + shift2x * 3.437f) * 5.0f;
-    wave = wave + ocn_sin((px * 0.03112f + py * 0.01122f) + shift2x * 4.269f) * 2.5f;
+    wave = wave + ocn_sin_pi(px * 0.021f + shift2x) * 4.5f;
+    wave = wave + ocn_sin_pi((px * 0.0172f + py * 0.010f) + shift2x * 1.121f) * 4.0f;
+    wave = wave - ocn_sin_pi((px * 0.00104f + py * 0.005f) + shift2x * 0.121f) * 4.0f;
+    wave = wave + ocn_sin_pi((px * 0.02221f + py * 0.01233f) + shift2x * 3.437f) * 5.0f;
+    wave = wave + ocn_sin_pi((px * 0.03112f + py * 0.01122f) + shift2x * 4.269f) * 2.5f;
     wave = wave * 1.0f; /* large_waveheight */
     height = height + wave;
     return height;
