@@ -177,3 +177,34 @@ def batch_of(scene_fn, B, **kw):
     takes_seed = "seed" in scene_fn.__code__.co_varnames
     frames = [scene_fn(seed=seed0 + b, **kw) if takes_seed else scene_fn(**kw) for b in range(B)]
     return tuple(np.stack([fr[k] for fr in frames]) for k in range(4))
+
+
+def deferred_mesh_scene(W=512, H=512, C=7, n=100, seed=0):
+    """BASELINE config 4 (samples/deferred.py:63-91 G-buffer): a shared-vertex, subdivided n x n grid surface
+    (2 (n-1)^2 ~ 20k triangles at n=100) rippled in depth, seen in perspective, carrying 7 channels per
+    vertex (normal xyz, albedo rgb, view depth) -- one 7-channel call instead of the reference's 3+3+1."""
+    rng = np.random.default_rng(seed)
+    u, v = np.meshgrid(np.linspace(-1.0, 1.0, n), np.linspace(-1.0, 1.0, n))
+    height = 0.15 * np.sin(3.0 * u) * np.cos(2.0 * v) + 0.02 * rng.standard_normal(u.shape)
+    world = np.stack([u * 1.6, height, v * 1.6 - 0.2], -1).reshape(-1, 3).astype(np.float32)
+    faces = []
+    for r in range(n - 1):
+        for c in range(n - 1):
+            a = r * n + c
+            faces.append([a, a + 1, a + n])
+            faces.append([a + 1, a + n + 1, a + n])
+    faces = np.array(faces, np.int32)
+    wt = torch.from_numpy(world)
+    ft = torch.from_numpy(faces).long()
+    normals = lighting.vertex_normals(wt, ft).numpy()
+    # tilted-plane perspective built directly in clip space: NDC x, y over [-0.9, 0.9] (plus the ripple),
+    # w grows from 1 at the bottom edge to 3 at the top (receding surface)
+    w = (2.0 + v).reshape(-1, 1)
+    ndc = np.stack([u * 0.9, v * 0.9 + height * 0.5], -1).reshape(-1, 2)
+    zc = (0.2 * v + height).reshape(-1, 1)
+    clip = np.concatenate([ndc * w, zc * w, w], 1).astype(np.float32)
+    albedo = rng.uniform(0.2, 1.0, size=(len(world), 3))
+    depth = w
+    attrs = np.concatenate([normals, albedo, depth], 1)[:, :C].astype(np.float32)
+    bg = np.zeros((H, W, C), np.float32)
+    return bg, clip, attrs, faces

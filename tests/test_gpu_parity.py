@@ -239,3 +239,22 @@ def test_two_process_frame_sharding_on_gpu():
         assert p.exitcode == 0
     for rank, lo, hi, full in res:
         np.testing.assert_array_equal(full, ref)
+
+
+def test_config4_deferred_gbuffer_7_channels():
+    """BASELINE config 4 (512x512x7, ~20k-triangle shared-vertex mesh in perspective): one 7-channel
+    call (the reference needs 3+3+1, samples/deferred.py:63-91)."""
+    check_scene(*scenes.deferred_mesh_scene())
+
+
+@pytest.mark.parametrize("H,W", [(40, 8192), (8192, 24)])
+def test_maximum_frame_dimensions(H, W):
+    """DIRT_MAX_DIM = 8192 along each axis: tile, coarse-bin and row-flip indexing at the extremes."""
+    bg, v, c, f = scenes.random_triangles(F=3000, W=W, H=H, radius_px=10.0, seed=12)
+    check_scene(bg, v, c, f)
+
+
+def test_large_triangle_stress_r64():
+    """SURVEY 8d stress variant (r = 64 px) at full 1024^2 with fewer faces: big bins, records spanning
+    many coarse tiles (workgroup-cooperative binning), large-edge records in the backward."""
+    check_scene(*scenes.random_triangles(F=4000, W=1024, H=1024, radius_px=64.0, seed=6))
