@@ -17,6 +17,10 @@ DIRT_EHIP = 3
 
 SHADER_GOURAUD = 0
 SHADER_OCEANIC_HORIZON = 1
+SHADER_OCEANIC = 2
+SHADER_OCEANIC_STILL_CLOUD = 3
+SHADER_OCEANIC_NO_CLOUD = 4
+SHADER_OCEANIC_SIMPLE_PROXY = 5
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192

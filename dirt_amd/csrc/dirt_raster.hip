@@ -675,7 +675,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                                                      int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
                                                      int32_t *__restrict__ gbuffer, float *__restrict__ zero_a,
                                                      int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
-                                                     const float *__restrict__ verts, const float *__restrict__ cam)
+                                                     const float *__restrict__ verts, const float *__restrict__ cam,
+                                                     int sid)
 {
     if (!(AB & 16)) {
         // housekeeping spread over all blocks (a few KB each): return fill's bin cursors to zero for
@@ -866,6 +867,23 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         const ocean::Camera camv{cam[0], cam[1], cam[2], cam[3], cam[4], cam[5], cam[6], cam[7]};
         const float2 col = ocean::shade(tx + sx / (float)W, ty + sy / (float)H, camv, (float)W, (float)H);
         for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 3 ? 1.0f : 0.0f;
+    } else if constexpr (SH == DIRT_SHADER_OCEANIC) {
+        // the oceanic family (shader ids 2..5, `sid` at run time), same texCoordV and jitter as above
+        const float *vb = verts + (int64_t)b * V * 4;
+        const float *p0 = vb + (int64_t)fd.v[0] * 4, *p1 = vb + (int64_t)fd.v[1] * 4, *p2 = vb + (int64_t)fd.v[2] * 4;
+        const float tx = (lam[0] * p0[0] + lam[1] * p1[0]) + lam[2] * p2[0];
+        const float ty = (lam[0] * p0[1] + lam[1] * p1[1]) + lam[2] * p2[1];
+        const float u = (tx + 1.0f) / 2.0f, v = (ty + 1.0f) / 2.0f;
+        int ix = (int)floorf(u * (float)W), iy = (int)floorf(v * (float)H);
+        if (!(u * (float)W >= 0.0f)) ix = 0;
+        if (!(v * (float)H >= 0.0f)) iy = 0;
+        ix = ix < 0 ? 0 : (ix > W - 1 ? W - 1 : ix);
+        iy = iy < 0 ? 0 : (iy > H - 1 ? H - 1 : iy);
+        const float *texel = background + (((int64_t)b * H + (H - 1 - iy)) * W + ix) * C;
+        const float sx = texel[0], sy = C >= 2 ? texel[1] : texel[0];
+        const float3 col = ocean::shade_family(ocean::family_params(sid), tx + sx / (float)W, ty + sy / (float)H, cam,
+                                               (float)W, (float)H);
+        for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 2 ? col.z : k == 3 ? 1.0f : 0.0f;
     } else {
         const float *cb = colors + (int64_t)b * V * C;
         const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
@@ -1575,10 +1593,10 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
 {
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
-    if (shader_id != DIRT_SHADER_GOURAUD && shader_id != DIRT_SHADER_OCEANIC_HORIZON)
+    if (shader_id < DIRT_SHADER_GOURAUD || shader_id > DIRT_SHADER_OCEANIC_SIMPLE_PROXY)
         return fail(DIRT_EINVAL, "Rasterise: unsupported shader_id");
-    if (shader_id == DIRT_SHADER_OCEANIC_HORIZON && !camera_pos)
-        return fail(DIRT_EINVAL, "Rasterise: the oceanic_horizon program needs camera_pos (8 floats)");
+    if (shader_id != DIRT_SHADER_GOURAUD && !camera_pos)
+        return fail(DIRT_EINVAL, "Rasterise: procedural fragment programs need camera_pos (8 floats, 9 for still_cloud)");
     if (B == 0) return DIRT_OK;
     if (!background || !pixels || !gbuffer || !saved || !scratch || (F > 0 && (!faces || !vertices)) ||
         (V > 0 && (!vertices || !vertex_colors)))
@@ -1623,13 +1641,17 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
+#define LAUNCH_PROC(CC, SHT)                                                                                     \
+    raster_kernel<CC, 0, SHT><<<grid, dim3(256), 0, stream>>>(                                                   \
+        background, vertex_colors, recs, fdata, ccursor, coffset, bins, L.bin_capacity, B, H, W, C, V, F, L.ntx,   \
+        L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices,                                  \
+        zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                      \
+        zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id)
 #define LAUNCH_RASTER(CC)                                                                                        \
     if (shader_id == DIRT_SHADER_OCEANIC_HORIZON)                                                                \
-        raster_kernel<CC, 0, DIRT_SHADER_OCEANIC_HORIZON><<<grid, dim3(256), 0, stream>>>(                       \
-            background, vertex_colors, recs, fdata, ccursor, coffset, bins, L.bin_capacity, B, H, W, C, V, F,      \
-            L.ntx, L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices,                       \
-            zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
-            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos);                               \
+        LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC_HORIZON);                                                            \
+    else if (shader_id >= DIRT_SHADER_OCEANIC)                                                                   \
+        LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC);                                                                    \
     else                                                                                                         \
     raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,   \
                                                       bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift,    \
@@ -1637,11 +1659,12 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
                                                       zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
                                                       zero_grad_vertex_colors,                                     \
                                                       zero_grad_vertex_colors ? (int64_t)B * V * C : 0,            \
-                                                      vertices, camera_pos)
+                                                      vertices, camera_pos, shader_id)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else LAUNCH_RASTER(0);
 #undef LAUNCH_RASTER
+#undef LAUNCH_PROC
     HIP_TRY(hipGetLastError());
     return DIRT_OK;
 }
@@ -1716,7 +1739,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
         raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,\
                                                              bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift, \
                                                              L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, 0,  \
-                                                             nullptr, 0, nullptr, nullptr);                         \
+                                                             nullptr, 0, nullptr, nullptr, 0);                      \
         break
     switch (variant) {
         V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8);

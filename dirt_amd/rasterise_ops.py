@@ -119,8 +119,10 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
         camera_pos = _as_tensor(camera_pos, torch.float32, dev).contiguous().reshape(-1)
         if camera_pos.numel() < 8:
             raise ValueError("camera_pos must hold at least 8 floats (csrc/rasterise_egl.cpp:323)")
-    elif shader_id == _lib.SHADER_OCEANIC_HORIZON:
-        raise ValueError("the oceanic_horizon fragment program needs camera_pos (8 floats)")
+        if shader_id == _lib.SHADER_OCEANIC_STILL_CLOUD and camera_pos.numel() < 9:
+            raise ValueError("oceanic_still_cloud reads cloud_t from camera_pos[8] (csrc/oceanic_still_cloud.cpp:407)")
+    elif shader_id != _lib.SHADER_GOURAUD:
+        raise ValueError("procedural fragment programs need camera_pos (8 floats)")
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
     pixels, gbuffer = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos,
                                                int(height), int(width), int(channels), shader_id, int(bin_capacity))
@@ -128,14 +130,17 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
 
 
 _SHADERS = {None: _lib.SHADER_GOURAUD, "gouraud": _lib.SHADER_GOURAUD,
-            "oceanic_horizon": _lib.SHADER_OCEANIC_HORIZON}
+            "oceanic_horizon": _lib.SHADER_OCEANIC_HORIZON, "oceanic": _lib.SHADER_OCEANIC,
+            "oceanic_still_cloud": _lib.SHADER_OCEANIC_STILL_CLOUD, "oceanic_no_cloud": _lib.SHADER_OCEANIC_NO_CLOUD,
+            "oceanic_simple_proxy": _lib.SHADER_OCEANIC_SIMPLE_PROXY}
 
 
 def _shader_id(shader):
     if isinstance(shader, int) and shader in _SHADERS.values():
         return shader
     if shader not in _SHADERS:
-        raise ValueError("unknown fragment program %r (expected 'gouraud' or 'oceanic_horizon')" % (shader,))
+        raise ValueError("unknown fragment program %r (expected one of %s)"
+                         % (shader, sorted(k for k in _SHADERS if k is not None)))
     return _SHADERS[shader]
 
 
@@ -197,19 +202,31 @@ def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None,
                               _shader_id(shader))
 
 
-def _procedural(opname):
+def _procedural_op(opname, shader, ref):
+    def op(background, vertices, vertex_colors, faces, camera_pos, height=None, width=None, channels=None,
+           name=None):
+        return rasterise(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, name,
+                         shader=shader)
+    op.__name__ = opname
+    op.__doc__ = ("Reference dirt/rasterise_ops.py `%s` (%s): `rasterise` with the `%s` fragment program "
+                  "(DESIGN.md 3b); forward only, like the reference." % (opname, ref, shader))
+    return op
+
+
+def _not_yet(opname):
     def op(background, vertices, vertex_colors, faces, camera_pos, height=None, width=None, channels=None,
            name=None):
         raise NotImplementedError(
             "%s: procedural fragment program not implemented yet on MI355X (SURVEY 8f-4)" % opname)
     op.__name__ = opname
-    op.__doc__ = "Reference dirt/rasterise_ops.py procedural op `%s` (SURVEY 8f-4)." % opname
+    op.__doc__ = "Reference dirt/rasterise_ops.py procedural op `%s` (SURVEY 8f-4), not built yet." % opname
     return op
 
 
-rasterise_grad = _procedural("rasterise_grad")
-oceanic_no_cloud = _procedural("oceanic_no_cloud")
-oceanic_simple_proxy = _procedural("oceanic_simple_proxy")
-oceanic_still_cloud = _procedural("oceanic_still_cloud")
-oceanic_opt_flow = _procedural("oceanic_opt_flow")
-hill = _procedural("hill")
+# RasteriseGrad binds the `oceanic` program (csrc/rasterise_grad_egl.cpp:399, SURVEY F4: not a gradient)
+rasterise_grad = _procedural_op("rasterise_grad", "oceanic", "rasterise_ops.py:91-108")
+oceanic_no_cloud = _procedural_op("oceanic_no_cloud", "oceanic_no_cloud", "rasterise_ops.py:110-127")
+oceanic_simple_proxy = _procedural_op("oceanic_simple_proxy", "oceanic_simple_proxy", "rasterise_ops.py:129-146")
+oceanic_still_cloud = _procedural_op("oceanic_still_cloud", "oceanic_still_cloud", "rasterise_ops.py:148-165")
+oceanic_opt_flow = _not_yet("oceanic_opt_flow")
+hill = _not_yet("hill")

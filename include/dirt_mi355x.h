@@ -52,7 +52,11 @@ extern "C" {
 
 /* fragment programs (shader_id); 0 = Gouraud (README.md:134-137) */
 #define DIRT_SHADER_GOURAUD 0
-#define DIRT_SHADER_OCEANIC_HORIZON 1 /* csrc/shaders.cpp:1668-1919 (the fork's bound program) */
+#define DIRT_SHADER_OCEANIC_HORIZON 1 /* csrc/shaders.cpp:1668-1919 (the fork's `Rasterise` program) */
+#define DIRT_SHADER_OCEANIC 2             /* csrc/shaders.cpp:556-864 (`RasteriseGrad`, rasterise_grad_egl.cpp:399) */
+#define DIRT_SHADER_OCEANIC_STILL_CLOUD 3 /* csrc/shaders.cpp:866-1176 (`OceanicStillCloud`; camera_pos[8] = cloud_t) */
+#define DIRT_SHADER_OCEANIC_NO_CLOUD 4    /* csrc/shaders.cpp:1402-1666 (`OceanicNoCloud`) */
+#define DIRT_SHADER_OCEANIC_SIMPLE_PROXY 5 /* csrc/shaders.cpp:1921-2185 (`OceanicSimpleProxy`) */
 
 /* ABI version, bumped on any signature change */
 int dirt_abi_version(void);
@@ -65,7 +69,8 @@ int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_c
 /* Forward: pixels = Rasterise(background, vertices, vertex_colors, faces).
  * gbuffer [B,H,W] int32 receives the per-pixel visible setup-record index (-1 = background),
  * which together with `saved` is what dirt_rasterise_bwd consumes.
- * camera_pos: device pointer to >= 8 floats, used only by shader_id != 0 (may be NULL for Gouraud). */
+ * camera_pos: device pointer to >= 8 floats (9 for DIRT_SHADER_OCEANIC_STILL_CLOUD), used only by the
+ * procedural programs (shader_id != 0; may be NULL for Gouraud). */
 int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
                        const int32_t *faces, const float *camera_pos,
                        int B, int H, int W, int C, int V, int F, int shader_id,

@@ -454,6 +454,308 @@ static void ocn_shade(float xyx, float xyy, const float *cam, float width, float
     out[1] = (0.5f * ocn_pow01(sundot, 10.0f) + 0.25f * ocn_pow01(sundot, 3.5f)) + 0.75f * ocn_pow01(sundot, 300.0f);
 }
 
+/* ------------------------------------------------------------------------------------------------ */
+/* The `oceanic` family: `oceanic` (bound by RasteriseGrad, shaders.cpp:556-864),
+ * `oceanic_still_cloud` (:866-1176), `oceanic_no_cloud` (:1402-1666) and `oceanic_simple_proxy`
+ * (:1921-2185) are one program with different constants, wave function, loop counts and cloud mode
+ * (the diffs of those four GLSL sources).  Same rules as above: GLSL operation order in float32, no
+ * contraction, the fixed transcendentals; mat*vec as (c0*x + c1*y) + c2*z over the columns; v *= M as
+ * the row-vector product; mix(a,b,t) = a*(1-t) + b*t; smoothstep per the GLSL definition; fract(x) =
+ * x - floor(x); exp(x) = exp2(x * log2(e)); pow(x,y) = exp2(y * log2(x)) for x > 0, 0 for x <= 0.  The
+ * god-ray term (RENDER_GODRAYS undefined) is the exact zero `vec3(..)*fog` and is omitted. */
+
+typedef struct {
+    float wavegain, large_wh, small_wh;
+    float fogcolor[3], skybottom[3], skytop[3], reflskycolor[3], watercolor[3];
+    float s1x, s1y, s2x, s2y; /* shift1 = 0.001*vec2(time*s1x*2, time*s1y*2), shift2 = 0.001*vec2(time*s2x*2, -time*s2y*2) */
+    int wave_cos;             /* large waves use cos (simple_proxy) instead of sin */
+    int small_iters;          /* 7, or 3 (simple_proxy) */
+    int march_steps;          /* 20, or 10 (simple_proxy) */
+    int clouds;               /* 0 none (trace_fog = 1), 1 moving with the camera (time), 2 still (cloud_t) */
+} ocn_family;
+
+static const ocn_family OCN_OCEANIC = {1.0f, 1.0f, 1.0f, {0.5f, 0.7f, 1.1f}, {0.6f, 0.8f, 1.2f}, {0.05f, 0.2f, 0.5f},
+                                       {0.025f, 0.10f, 0.20f}, {0.2f, 0.25f, 0.3f}, 160.0f, 120.0f, 190.0f, 130.0f,
+                                       0, 7, 20, 1};
+static const ocn_family OCN_STILL = {1.0f, 1.0f, 1.0f, {0.5f, 0.7f, 1.1f}, {0.6f, 0.8f, 1.2f}, {0.05f, 0.2f, 0.5f},
+                                     {0.025f, 0.10f, 0.20f}, {0.2f, 0.25f, 0.3f}, 160.0f, 120.0f, 190.0f, 130.0f,
+                                     0, 7, 20, 2};
+static const ocn_family OCN_NOCLOUD = {1.0f, 1.0f, 1.0f, {0.5f, 0.7f, 1.1f}, {0.6f, 0.8f, 1.2f}, {0.05f, 0.2f, 0.5f},
+                                       {0.025f, 0.10f, 0.20f}, {0.2f, 0.25f, 0.3f}, 160.0f, 120.0f, 190.0f, 130.0f,
+                                       0, 7, 20, 0};
+static const ocn_family OCN_PROXY = {0.75f, 0.75f, 1.5f, {0.4f, 0.4f, 1.2f}, {0.5f, 0.5f, 1.3f}, {0.15f, 0.1f, 0.7f},
+                                     {0.1f, 0.1f, 0.15f}, {0.1f, 0.2f, 0.5f}, 260.0f, 100.0f, 150.0f, 230.0f,
+                                     1, 3, 10, 0};
+
+static float ocn_fract(float x) { return x - floorf(x); }
+static float ocn_mix(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+static float ocn_smoothstep(float e0, float e1, float x)
+{
+    const float t = ocn_clamp01((x - e0) / (e1 - e0));
+    return t * t * (3.0f - 2.0f * t);
+}
+static float ocn_exp2_any(float z)
+{
+    if (!(z >= -125.0f)) return 0.0f; /* also NaN */
+    if (z > 128.0f) return INFINITY;
+    const float n = floorf(z + 0.5f);
+    const float f = z - n;
+    const float p = 1.0f + f * (0.6931471806f + f * (0.2402265070f + f * (0.05550410866f + f * (0.009618129108f +
+                    f * (0.001333355815f + f * 0.0001540353039f)))));
+    return ldexpf(p, (int)n);
+}
+static float ocn_pow_pos(float x, float y) /* GLSL pow for any x (0 for x <= 0) */
+{
+    if (!(x >= 1.17549435e-38f)) return 0.0f;
+    if (x == 1.0f) return 1.0f;
+    if (!(x < INFINITY)) return INFINITY;
+    return ocn_exp2_any(y * ocn_log2(x));
+}
+static float ocn_exp(float x) { return ocn_exp2_any(x * 1.44269504f); }
+
+static float ocn_hash(float n) { return ocn_fract(ocn_cos(n) * 41415.92653f); }
+static float ocn_rand2(float nx, float ny) { return ocn_fract(ocn_sin_pi(nx * 12.9898f + ny * 4.1414f) * 43758.5453f); }
+
+static float ocn_noise2(float px, float py)
+{
+    const float ix = floorf(px), iy = floorf(py);
+    float ux = ocn_fract(px), uy = ocn_fract(py);
+    ux = ux * ux * (3.0f - 2.0f * ux);
+    uy = uy * uy * (3.0f - 2.0f * uy);
+    return ocn_mix(ocn_mix(ocn_rand2(ix, iy), ocn_rand2(ix + 1.0f, iy + 0.0f), ux),
+                   ocn_mix(ocn_rand2(ix + 0.0f, iy + 1.0f), ocn_rand2(ix + 1.0f, iy + 1.0f), ux), uy);
+}
+
+static float ocn_noise3(float x, float y, float z)
+{
+    const float px = floorf(x), py = floorf(y), pz = floorf(z);
+    const float fx = ocn_smoothstep(0.0f, 1.0f, ocn_fract(x));
+    const float fy = ocn_smoothstep(0.0f, 1.0f, ocn_fract(y));
+    const float fz = ocn_smoothstep(0.0f, 1.0f, ocn_fract(z));
+    const float n = (px + py * 57.0f) + 113.0f * pz;
+    return ocn_mix(ocn_mix(ocn_mix(ocn_hash(n + 0.0f), ocn_hash(n + 1.0f), fx),
+                           ocn_mix(ocn_hash(n + 57.0f), ocn_hash(n + 58.0f), fx), fy),
+                   ocn_mix(ocn_mix(ocn_hash(n + 113.0f), ocn_hash(n + 114.0f), fx),
+                           ocn_mix(ocn_hash(n + 170.0f), ocn_hash(n + 171.0f), fx), fy), fz);
+}
+
+/* mat3 m = mat3(0.00,1.60,1.20, -1.60,0.72,-0.96, -1.20,-0.96,1.28) (columns), m*p */
+static void ocn_m3(float p[3])
+{
+    const float x = p[0], y = p[1], z = p[2];
+    p[0] = (0.00f * x + -1.60f * y) + -1.20f * z;
+    p[1] = (1.60f * x + 0.72f * y) + -0.96f * z;
+    p[2] = (1.20f * x + -0.96f * y) + 1.28f * z;
+}
+
+static float ocn_fbm3(float x, float y, float z)
+{
+    float p[3] = {x, y, z};
+    float f = 0.5000f * ocn_noise3(p[0], p[1], p[2]);
+    ocn_m3(p); p[0] = p[0] * 1.1f; p[1] = p[1] * 1.1f; p[2] = p[2] * 1.1f;
+    f = f + 0.2500f * ocn_noise3(p[0], p[1], p[2]);
+    ocn_m3(p); p[0] = p[0] * 1.2f; p[1] = p[1] * 1.2f; p[2] = p[2] * 1.2f;
+    f = f + 0.1666f * ocn_noise3(p[0], p[1], p[2]);
+    ocn_m3(p);
+    f = f + 0.0834f * ocn_noise3(p[0], p[1], p[2]);
+    return f;
+}
+
+/* mat2 m2 = mat2(1.6,-1.2, 1.2,1.6) (columns), m2*p */
+static float ocn_fbm2(float x, float y)
+{
+    float f = 0.5000f * ocn_noise2(x, y);
+    float nx = 1.6f * x + 1.2f * y, ny = -1.2f * x + 1.6f * y; x = nx; y = ny;
+    f = f + 0.2500f * ocn_noise2(x, y);
+    nx = 1.6f * x + 1.2f * y; ny = -1.2f * x + 1.6f * y; x = nx; y = ny;
+    f = f + 0.1666f * ocn_noise2(x, y);
+    nx = 1.6f * x + 1.2f * y; ny = -1.2f * x + 1.6f * y; x = nx; y = ny;
+    f = f + 0.0834f * ocn_noise2(x, y);
+    return f;
+}
+
+static float ocn_family_water(const ocn_family *P, float px, float py, float time)
+{
+    float height = 70.0f;
+    float s1x = 0.001f * ((time * P->s1x) * 2.0f), s1y = 0.001f * ((time * P->s1y) * 2.0f);
+    const float s2x = 0.001f * ((time * P->s2x) * 2.0f), s2y = 0.001f * ((-time * P->s2y) * 2.0f);
+    float wave = 0.0f;
+    if (P->wave_cos) {
+        wave = wave + ocn_cos(px * 0.021f + s2x) * 4.5f;
+        wave = wave + ocn_cos((px * 0.0172f + py * 0.010f) + s2x * 1.121f) * 4.0f;
+        wave = wave - ocn_cos((px * 0.00104f + py * 0.005f) + s2x * 0.121f) * 4.0f;
+        wave = wave + ocn_cos((px * 0.02221f + py * 0.01233f) + s2x * 3.437f) * 5.0f;
+        wave = wave + ocn_cos((px * 0.03112f + py * 0.01122f) + s2x * 4.269f) * 2.5f;
+    } else {
+        wave = wave + ocn_sin_pi(px * 0.021f + s2x) * 4.5f;
+        wave = wave + ocn_sin_pi((px * 0.0172f + py * 0.010f) + s2x * 1.121f) * 4.0f;
+        wave = wave - ocn_sin_pi((px * 0.00104f + py * 0.005f) + s2x * 0.121f) * 4.0f;
+        wave = wave + ocn_sin_pi((px * 0.02221f + py * 0.01233f) + s2x * 3.437f) * 5.0f;
+        wave = wave + ocn_sin_pi((px * 0.03112f + py * 0.01122f) + s2x * 4.269f) * 2.5f;
+    }
+    wave = wave * P->large_wh;
+    wave = wave - (ocn_fbm2(px * 0.004f - s2x * 0.5f, py * 0.004f - s2y * 0.5f) * P->small_wh) * 24.0f;
+    float amp = 6.0f * P->small_wh;
+    s1x = s1x * 0.3f; s1y = s1y * 0.3f;
+    const float m00 = 1.6f * 0.9331f, m01 = -1.2f * 0.9331f, m10 = 1.2f * 0.9331f, m11 = 1.6f * 0.9331f;
+    for (int i = 0; i < P->small_iters; ++i) {
+        wave = wave - fabsf(ocn_sin_pi((ocn_noise2(px * 0.01f + s1x, py * 0.01f + s1y) - 0.5f) * 3.14f)) * amp;
+        amp = amp * 0.51f;
+        s1x = s1x * 1.841f; s1y = s1y * 1.841f;
+        const float nx = px * m00 + py * m01, ny = px * m10 + py * m11; /* p *= m2*0.9331 (row vector) */
+        px = nx; py = ny;
+    }
+    height = height + wave;
+    return height;
+}
+/* trace_fog (cloud cover along a ray, 10 layers; 1 without clouds) */
+static float ocn_family_trace_fog(const ocn_family *P, const float ro[3], const float rd[3], const float *cam)
+{
+    if (P->clouds == 0) return 1.0f;
+    const float ct = P->clouds == 2 ? cam[8] : cam[6];
+    const float shx = ct * 80.0f, shy = ct * 60.0f;
+    float sum = 0.0f, q2 = 0.0f, q3 = 0.0f;
+    for (int q = 0; q < 10; ++q) {
+        float cx, cy, cz;
+        if (P->clouds == 1) {
+            const float c = ((q2 + 350.0f) - ro[1]) / rd[1];
+            cx = (ro[0] + c * rd[0]) + 831.0f;
+            cy = (ro[1] + c * rd[1]) + ((321.0f + q3) - shx * 0.2f);
+            cz = (ro[2] + c * rd[2]) + (1330.0f + shy * 3.0f);
+        } else {
+            const float c = (q2 + 350.0f) / rd[1];
+            cx = c * rd[0] + 831.0f;
+            cy = c * rd[1] + ((321.0f + q3) - shx * 0.2f);
+            cz = c * rd[2] + (1330.0f + shy * 3.0f);
+        }
+        const float alpha = ocn_smoothstep(0.5f, 1.0f, ocn_fbm3(cx * 0.0015f, cy * 0.0015f, cz * 0.0015f));
+        sum = sum + (1.0f - sum) * alpha;
+        if (sum > 0.98f) break;
+        q2 = q2 + 120.0f;
+        q3 = q3 + 0.15f;
+    }
+    return ocn_clamp01(1.0f - sum);
+}
+
+/* main() of the family: writes col.xyz */
+static void ocn_family_shade(const ocn_family *P, float xyx, float xyy, const float *cam, float width, float height,
+                             float out[3])
+{
+    const float ro[3] = {cam[0], cam[1], cam[2]};
+    const float time = cam[6];
+    float light[3] = {0.1f, 0.25f, cam[7]};
+    ocn_normalize(light);
+    float rdv[3];
+    rdv[0] = (xyx + 1.0f) * width / 2.0f - width / 2.0f;
+    rdv[1] = (xyy + 1.0f) * height / 2.0f - height / 2.0f;
+    rdv[2] = 1.73f * width / 2.0f;
+    ocn_normalize(rdv);
+    const float sin1 = ocn_sin(cam[3]), cos1 = ocn_cos(cam[3]);
+    const float sin2 = ocn_sin(cam[4]), cos2 = ocn_cos(cam[4]);
+    const float sin3 = ocn_sin(cam[5]), cos3 = ocn_cos(cam[5]);
+    float rd[3];
+    rd[0] = ((cos2 * cos3) * rdv[0] + (-cos1 * sin3 + (sin1 * sin2) * cos3) * rdv[1]) +
+            (sin1 * sin3 + (cos1 * sin2) * cos3) * rdv[2];
+    rd[1] = ((cos2 * sin3) * rdv[0] + (cos1 * cos3 + (sin1 * sin2) * sin3) * rdv[1]) +
+            (-sin1 * cos3 + (cos1 * sin2) * sin3) * rdv[2];
+    rd[2] = (-sin2 * rdv[0] + (sin1 * cos2) * rdv[1]) + (cos1 * cos2) * rdv[2];
+    const float sundot = ocn_clamp01(ocn_dot3(rd, light));
+    if (rd[1] > 0.0f) {
+        /* sky (trace() returns false; its march is not read) */
+        const float t = ocn_pow_pos(1.0f - 0.7f * rd[1], 15.0f);
+        float col[3];
+        const float p350 = ocn_pow_pos(sundot, 350.0f), p2 = ocn_pow_pos(sundot, 2.0f);
+        const float sunc[3] = {0.47f * 1.6f, 0.47f * 1.4f, 0.47f * 1.0f}, haze[3] = {0.4f * 0.8f, 0.4f * 0.9f, 0.4f * 1.0f};
+        for (int k = 0; k < 3; ++k) {
+            col[k] = 0.8f * (P->skybottom[k] * t + P->skytop[k] * (1.0f - t));
+            col[k] = col[k] + sunc[k] * p350;
+            col[k] = col[k] + haze[k] * p2;
+        }
+        if (P->clouds != 0) {
+            const float ct = P->clouds == 2 ? cam[8] : time;
+            const float shx = ct * 80.0f, shy = ct * 60.0f;
+            float sum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            const float dense[3] = {0.7f * 0.4f, 0.7f * 0.4f, 0.7f * 0.3f}, light_c[3] = {1.1f, 1.05f, 1.0f};
+            for (int q = 1000; q < 1100; ++q) {
+                const float fq = (float)(q - 1000);
+                float cx, cy, cz;
+                if (P->clouds == 1) {
+                    const float c = ((fq * 12.0f + 350.0f) - cam[1]) / rd[1];
+                    cx = (ro[0] + c * rd[0]) + 831.0f;
+                    cy = (ro[1] + c * rd[1]) + ((321.0f + fq * 0.15f) - shx * 0.2f);
+                    cz = (ro[2] + c * rd[2]) + (1330.0f + shy * 3.0f);
+                } else {
+                    const float c = (fq * 12.0f + 350.0f) / rd[1];
+                    cx = c * rd[0] + 831.0f;
+                    cy = c * rd[1] + ((321.0f + fq * 0.15f) - shx * 0.2f);
+                    cz = c * rd[2] + (1330.0f + shy * 3.0f);
+                }
+                float alpha = ocn_smoothstep(0.5f, 1.0f, ocn_fbm3(cx * 0.0015f, cy * 0.0015f, cz * 0.0015f)) * 0.9f;
+                float lc[3];
+                for (int k = 0; k < 3; ++k) lc[k] = ocn_mix(light_c[k], dense[k], alpha);
+                alpha = (1.0f - sum[3]) * alpha;
+                for (int k = 0; k < 3; ++k) sum[k] = sum[k] + lc[k] * alpha;
+                sum[3] = sum[3] + alpha;
+                if (sum[3] > 0.98f) break;
+            }
+            const float alpha = ocn_smoothstep(0.7f, 1.0f, sum[3]);
+            const float p13 = ocn_pow_pos(sundot, 13.0f), p5 = ocn_pow_pos(sundot, 5.0f);
+            const float shade_c[3] = {0.6f * 0.8f, 0.6f * 0.75f, 0.6f * 0.7f}, scat[3] = {0.2f * 1.3f, 0.2f * 1.2f, 0.2f * 1.0f};
+            for (int k = 0; k < 3; ++k) {
+                sum[k] = sum[k] / (sum[3] + 0.0001f);
+                sum[k] = sum[k] - (shade_c[k] * p13) * alpha;
+                sum[k] = sum[k] + (scat[k] * p5) * (1.0f - alpha);
+                col[k] = ocn_mix(col[k], sum[k], sum[3] * (1.0f - t));
+            }
+        }
+        out[0] = col[0]; out[1] = col[1]; out[2] = col[2];
+        return;
+    }
+    /* trace(), shaders.cpp:700-744 */
+    float t = -ro[1] / rd[1];
+    float st = 0.5f, old_h = 0.0f;
+    for (int j = 0; j < P->march_steps; ++j) {
+        if (t > 500.0f) st = 1.0f;
+        if (t > 800.0f) st = 2.0f;
+        if (t > 1500.0f) st = 3.0f;
+        const float p0 = ro[0] + t * rd[0], p1 = ro[1] + t * rd[1], p2 = ro[2] + t * rd[2];
+        const float h = p1 - ocn_family_water(P, p0, p2, time);
+        t = t + (fmaxf(1.0f, fabsf(h)) * ocn_sign(h)) * st;
+        if (old_h * h < 0.0f) st = st / 2.0f;
+        old_h = h;
+    }
+    const float dist = t;
+    const float wpos[3] = {ro[0] + dist * rd[0], ro[1] + dist * rd[1], ro[2] + dist * rd[2]};
+    const float d = 0.1f * P->wavegain * 4.0f;
+    float n[3] = {ocn_family_water(P, wpos[0] - d, wpos[2], time) - ocn_family_water(P, wpos[0] + d, wpos[2], time), 1.0f,
+                  ocn_family_water(P, wpos[0], wpos[2] - d, time) - ocn_family_water(P, wpos[0], wpos[2] + d, time)};
+    ocn_normalize(n);
+    const float dn = 2.0f * ocn_dot3(n, rd);
+    const float rr[3] = {rd[0] - dn * n[0], rd[1] - dn * n[1], rd[2] - dn * n[2]};
+    const float up[3] = {0.0f, 1.0f, 0.0f};
+    const float refl = 1.0f - ocn_clamp01(ocn_dot3(rr, up));
+    const float fro[3] = {wpos[0] + 20.0f * rr[0], wpos[1] + 20.0f * rr[1], wpos[2] + 20.0f * rr[2]};
+    const float sh = ocn_smoothstep(0.2f, 1.0f, ocn_family_trace_fog(P, fro, rr, cam)) * 0.7f + 0.3f;
+    const float wsky = refl * sh, wwater = (1.0f - refl) * sh;
+    const float sd = ocn_clamp01(ocn_dot3(rr, light));
+    const float lift = (wpos[1] - 70.0f) + 30.0f;
+    const float tint[3] = {0.003f, 0.005f, 0.005f};
+    const float wsunrefl = wsky * ((0.5f * ocn_pow_pos(sd, 10.0f) + 0.25f * ocn_pow_pos(sd, 3.5f)) +
+                                   0.75f * ocn_pow_pos(sd, 300.0f));
+    const float sunw[3] = {1.5f, 1.3f, 1.0f};
+    const float fo = 1.0f - ocn_exp(-ocn_pow_pos(0.0003f * dist, 1.5f));
+    const float p4 = ocn_pow_pos(sd, 4.0f);
+    const float fogc[3] = {0.6f * 0.6f, 0.6f * 0.5f, 0.6f * 0.4f};
+    for (int k = 0; k < 3; ++k) {
+        float c = wsky * P->reflskycolor[k];
+        c = c + wwater * P->watercolor[k];
+        c = c + tint[k] * lift;
+        c = c + sunw[k] * wsunrefl;
+        const float fco = P->fogcolor[k] + fogc[k] * p4;
+        out[k] = ocn_mix(c, fco, fo);
+    }
+}
+
 /* texCoordV = perspective-correct interpolation of the vertices' clip xy (shaders.cpp:19,21 alias
  * texCoord to position); jitter = background texel at (texCoordV+1)/2 (NEAREST; at texel centres the
  * reference's LINEAR magnification returns the same texel), channels x,y (C=1 broadcast,
@@ -470,6 +772,23 @@ void oracle_oceanic_horizon_pixel(const float *bgframe, int H, int W, int C, flo
     const float *texel = bgframe + (((int64_t)(H - 1 - iy)) * W + ix) * C;
     const float sx = texel[0], sy = C >= 2 ? texel[1] : texel[0];
     ocn_shade(tx + sx / (float)W, ty + sy / (float)H, cam, (float)W, (float)H, out);
+}
+
+/* shader ids 2..5 (include/dirt_mi355x.h): the oceanic family; writes col.xyz */
+void oracle_oceanic_family_pixel(int shader_id, const float *bgframe, int H, int W, int C, float tx, float ty,
+                                 const float *cam, float out[3])
+{
+    const ocn_family *P = shader_id == 2 ? &OCN_OCEANIC : shader_id == 3 ? &OCN_STILL
+                          : shader_id == 4 ? &OCN_NOCLOUD : &OCN_PROXY;
+    const float u = (tx + 1.0f) / 2.0f, v = (ty + 1.0f) / 2.0f;
+    int ix = (int)floorf(u * (float)W), iy = (int)floorf(v * (float)H);
+    if (!(u * (float)W >= 0.0f)) ix = 0;
+    if (!(v * (float)H >= 0.0f)) iy = 0;
+    ix = ix < 0 ? 0 : (ix > W - 1 ? W - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > H - 1 ? H - 1 : iy);
+    const float *texel = bgframe + (((int64_t)(H - 1 - iy)) * W + ix) * C;
+    const float sx = texel[0], sy = C >= 2 ? texel[1] : texel[0];
+    ocn_family_shade(P, tx + sx / (float)W, ty + sy / (float)H, cam, (float)W, (float)H, out);
 }
 
 int oracle_rasterise_fwd_shader(const float *background, const float *vertices, const float *vertex_colors,
@@ -548,6 +867,17 @@ int oracle_rasterise_fwd_shader(const float *background, const float *vertices, 
                     float lam[3] = {0.0f, 0.0f, 0.0f};
                     parent_lambda(r, E, lam);
                     const int32_t *f3 = fb + 3 * (int64_t)r->face;
+                    if (shader_id >= 2) {
+                        const float tx = (lam[0] * vb[(int64_t)f3[0] * 4] + lam[1] * vb[(int64_t)f3[1] * 4]) +
+                                         lam[2] * vb[(int64_t)f3[2] * 4];
+                        const float ty = (lam[0] * vb[(int64_t)f3[0] * 4 + 1] + lam[1] * vb[(int64_t)f3[1] * 4 + 1]) +
+                                         lam[2] * vb[(int64_t)f3[2] * 4 + 1];
+                        float col[3];
+                        oracle_oceanic_family_pixel(shader_id, background + (int64_t)b * H * W * C, H, W, C, tx, ty,
+                                                    camera_pos, col);
+                        for (int c = 0; c < C; ++c) out[c] = c < 3 ? col[c] : c == 3 ? 1.0f : 0.0f;
+                        continue;
+                    }
                     if (shader_id == 1) {
                         /* fragColor = (col.x, col.y, 0, 1) (shaders.cpp:1860-1862,1916) */
                         const float tx = (lam[0] * vb[(int64_t)f3[0] * 4] + lam[1] * vb[(int64_t)f3[1] * 4]) +

@@ -32,6 +32,8 @@ def load():
         lib.oracle_rasterise_fwd_shader.restype = I
         lib.oracle_oceanic_horizon_pixel.argtypes = [P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
         lib.oracle_oceanic_horizon_pixel.restype = None
+        lib.oracle_oceanic_family_pixel.argtypes = [I, P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
+        lib.oracle_oceanic_family_pixel.restype = None
         lib.oracle_rasterise_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, I]
         lib.oracle_rasterise_bwd.restype = I
         lib.oracle_max_threads.argtypes = []
@@ -62,9 +64,12 @@ def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0, shader
     V, F = vs.shape[1], fs.shape[1]
     pixels = np.empty((B, H, W, C), np.float32)
     gbuf = np.empty((B, H, W), np.int32)
-    cam = _f32(camera_pos if camera_pos is not None else np.zeros(8))
-    if shader_id == 1 and cam.size < 8:
-        raise ValueError("oceanic_horizon needs camera_pos with at least 8 floats")
+    cam = np.zeros(16, np.float32)
+    if camera_pos is not None:
+        c = _f32(camera_pos).reshape(-1)
+        cam[:c.size] = c
+        if shader_id >= 1 and c.size < (9 if shader_id == 3 else 8):
+            raise ValueError("procedural programs need camera_pos (8 floats, 9 for oceanic_still_cloud)")
     st = load().oracle_rasterise_fwd_shader(_ptr(bg), _ptr(vs), _ptr(cs), _ptr(fs), B, H, W, C, V, F, shader_id,
                                             _ptr(cam), _ptr(pixels), _ptr(gbuf), nthreads)
     return pixels, gbuf, st

@@ -78,3 +78,25 @@ def test_oceanic_horizon_uncovered_pixels_keep_background():
     assert unc.any() and (~unc).any()
     np.testing.assert_array_equal(px[0][unc], bg[unc])
     assert set(np.unique(px[0][~unc][:, 0])) <= {0.0, 1.0}
+
+
+FAMILY_CAMS = [[0.0, 150.0, 0.0, 0.0, 0.1, 0.0, 1.0, 0.9, 2.0], [5.0, 120.0, -20.0, 0.02, -0.15, 0.05, 3.0, 1.2, 0.5]]
+
+
+@pytest.mark.parametrize("sid", [2, 3, 4, 5], ids=["oceanic", "still_cloud", "no_cloud", "simple_proxy"])
+def test_oceanic_family_against_float64(sid):
+    """The `oceanic` family.  Its noise (hash = fract(cos(n)*41415.9), rand =
+    fract(sin(.)*43758.5)) turns any ulp difference into a different random value, so float64 pins
+    only what is noise-free: the sky of the cloudless members to 1e-4, and otherwise image statistics
+    (mean colour of the water and of the sky within 0.05)."""
+    H, W = 48, 72
+    for cam in FAMILY_CAMS:
+        px, gb, _ = oracle.rasterise_fwd(*fullscreen(H, W), shader_id=sid, camera_pos=np.array(cam))
+        ref, rdy = oceanic_f64.render_family_fullscreen(sid, H, W, cam)
+        sky = rdy > 1e-4
+        water = rdy < -1e-4
+        assert np.isfinite(px).all()
+        if sid in (4, 5):
+            assert np.abs(px[0][sky] - ref[sky]).max() <= 1e-4
+        assert np.abs(px[0][sky].mean(0) - ref[sky].mean(0)).max() <= 0.05
+        assert np.abs(px[0][water].mean(0) - ref[water].mean(0)).max() <= 0.05

@@ -16,8 +16,8 @@ from dirt_amd import _lib  # noqa: E402
 from dirt_amd.session import RasteriseSession  # noqa: E402
 
 
-def main(steps=200, H=640, W=960, B=1, pitch=0.0):
-    cam_np = np.array([0.0, 200.0, 0.0, pitch, 0.0, 0.0, 0.0, 0.9], np.float32)
+def main(steps=200, H=640, W=960, B=1, pitch=0.0, shader=1):
+    cam_np = np.array([0.0, 200.0, 0.0, pitch, 0.0, 0.0, 0.0, 0.9, 0.0], np.float32)
     bg = np.zeros((B, H, W, 3), np.float32)
     v = np.tile(np.array([[[-1, -1, 0, 1], [-1, 1, 0, 1], [1, 1, 0, 1], [1, -1, 0, 1]]], np.float32), (B, 1, 1))
     f = np.tile(np.array([[[0, 1, 2], [0, 2, 3]]], np.int32), (B, 1, 1))
@@ -25,7 +25,7 @@ def main(steps=200, H=640, W=960, B=1, pitch=0.0):
     dev = torch.device("cuda", 0)
     t = [torch.from_numpy(a).to(dev) for a in (bg, v, c, f)]
     cam = torch.from_numpy(cam_np).to(dev)
-    sess = RasteriseSession(B, H, W, 3, 4, 2, device=dev, shader_id=_lib.SHADER_OCEANIC_HORIZON)
+    sess = RasteriseSession(B, H, W, 3, 4, 2, device=dev, shader_id=shader)
     for _ in range(5):
         sess.forward(*t, camera_pos=cam)
     g = torch.cuda.CUDAGraph()
@@ -48,13 +48,15 @@ def main(steps=200, H=640, W=960, B=1, pitch=0.0):
     from oracle import oracle
     nth = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     c0 = time.perf_counter()
-    oracle.rasterise_fwd(bg, v, c, f, nthreads=nth, shader_id=1, camera_pos=cam_np)
+    oracle.rasterise_fwd(bg, v, c, f, nthreads=nth, shader_id=shader, camera_pos=cam_np)
     cpu = time.perf_counter() - c0
-    print(json.dumps({"metric": "Mpixels/s forward, oceanic_horizon 960x640 full-screen", "pitch": pitch, "value":
+    names = {1: "oceanic_horizon", 2: "oceanic", 3: "oceanic_still_cloud", 4: "oceanic_no_cloud",
+             5: "oceanic_simple_proxy"}
+    print(json.dumps({"metric": "Mpixels/s forward, %s 960x640 full-screen" % names[shader], "pitch": pitch, "value":
                       round(B * H * W / dt / 1e6, 1), "ms_per_frame": round(dt * 1e3 / B, 4),
                       "kernels_us": {k: round(ms / n * 1e3, 2) for k, (n, ms) in prof.items() if n},
                       "cpu_oracle": {"Mpixels/s": round(B * H * W / cpu / 1e6, 2), "threads": nth}}))
 
 
 if __name__ == "__main__":
-    main(pitch=float(sys.argv[1]) if len(sys.argv) > 1 else 0.0)
+    main(pitch=float(sys.argv[1]) if len(sys.argv) > 1 else 0.0, shader=int(sys.argv[2]) if len(sys.argv) > 2 else 1)
