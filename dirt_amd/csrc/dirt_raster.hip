@@ -981,6 +981,11 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
 #define DIRT_GRAD_ATTR
 #endif
 
+// window-transform constants of the chain rule, computed on the host (IEEE, as the oracle)
+struct NdcScale {
+    float inv_hw, inv_hh, half_w, half_h;
+};
+
 constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
 constexpr int kHaloPix = kHalo * kHalo;
 constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS (typ. 10-40)
@@ -1099,7 +1104,8 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                                                    const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
                                                    int V, int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
-                                                   float *__restrict__ grad_colors, float *__restrict__ grad_bg)
+                                                   float *__restrict__ grad_colors, float *__restrict__ grad_bg,
+                                                   const NdcScale ns)
 {
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     constexpr int CP = CM == 3 ? 4 : CM;  // LDS pixel stride (float4 for RGB)
@@ -1130,8 +1136,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
     // uniform: readfirstlane (convergent) keeps the divisions at the top instead of in every pair branch
-    const float inv_hw = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 2.0f / (float)W)));
-    const float inv_hh = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 2.0f / (float)H)));
+    const float inv_hw = ns.inv_hw, inv_hh = ns.inv_hh;  // 2/W, 2/H from the host (no division in the kernel)
     const int kme = (ly + 1) * kHalo + (lx + 1);
     const bool in_frame = i < W && j < H;
 
@@ -1397,7 +1402,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
             if (Wm == 0.0f) continue;
             const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
-            const float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
+            const float half = axis == 0 ? ns.half_w : ns.half_h;
             const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
             const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
             const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
@@ -1669,6 +1674,11 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     return DIRT_OK;
 }
 
+static NdcScale ndc_scale(int W, int H)
+{
+    return NdcScale{2.0f / (float)W, 2.0f / (float)H, 0.5f * (float)W, 0.5f * (float)H};
+}
+
 int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces, const float *pixels,
                        const float *grad_pixels, const int32_t *gbuffer, const void *saved, int B, int H, int W, int C,
                        int V, int F, float *grad_vertices, float *grad_vertex_colors, float *grad_background,
@@ -1703,7 +1713,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
 #define LAUNCH_GRAD(CC)                                                                                       \
     grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, recs, fdata, B, H, W, C, V, F, \
                                                     L.ntx, L.nrec, grad_vertices, grad_vertex_colors,            \
-                                                    grad_background)
+                                                    grad_background, ndc_scale(W, H))
     if (C == 1) LAUNCH_GRAD(1);
     else if (C == 3) LAUNCH_GRAD(3);
     else LAUNCH_GRAD(0);
@@ -1781,7 +1791,7 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     case AB:                                                                                                         \
         grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, recs, fdata, B, H, W, C, V, \
                                                            F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,     \
-                                                           grad_background);                                         \
+                                                           grad_background, ndc_scale(W, H));                        \
         break
     switch (variant) {
         V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);
