@@ -21,10 +21,12 @@ SHADER_OCEANIC = 2
 SHADER_OCEANIC_STILL_CLOUD = 3
 SHADER_OCEANIC_NO_CLOUD = 4
 SHADER_OCEANIC_SIMPLE_PROXY = 5
+SHADER_OCEANIC_OPT_FLOW = 6
+SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 BWD_ACCUMULATE = 1     # dirt_rasterise_bwd flags
@@ -40,6 +42,7 @@ SIGNATURES = {
     "dirt_workspace_sizes": (_I, [_I, _I, _I, _I, _I, _I, _I64, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "dirt_rasterise_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _U,
                                 _P, _P, _P]),
+    "dirt_hill_fwd": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _P]),
     "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _U, _P]),
     "dirt_scratch_clear": (_I, [_I, _I, _I, _I, _I64, _P, _SZ, _P]),
     "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),

@@ -31,7 +31,7 @@
 #include "../../include/dirt_mi355x.h"
 #include "raster_rules.h"
 #include "oceanic.h"
-#include "oceanic.h"
+#include "hill.h"
 
 using namespace dirt;
 
@@ -583,6 +583,8 @@ struct PixelState {
     int32_t best_rec;
 };
 
+// NoDepth: GL_DEPTH_TEST off (hill.cpp:194): the last face in draw order wins, near/far clipping stays
+template <bool NoDepth = false>
 __device__ __forceinline__ void depth_update(float za, float zb, float fx0, float fy0, float z0, int32_t face,
                                              int32_t ri, float fxl, float fyl, PixelState &st)
 {
@@ -590,8 +592,8 @@ __device__ __forceinline__ void depth_update(float za, float zb, float fx0, floa
     const float zw = (za * (fxl - fx0) + zb * (fyl - fy0)) + z0;
     if (!(zw >= 0.0f && zw <= 1.0f)) return;
     const uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
-    if (q >= kDepthMax) return;
-    const uint64_t key = ((uint64_t)q << 32) | (uint32_t)face;
+    if (!NoDepth && q >= kDepthMax) return;
+    const uint64_t key = NoDepth ? (uint64_t)(0xffffffffu - (uint32_t)face) : (((uint64_t)q << 32) | (uint32_t)face);
     if (key < st.best) {
         st.best = key;
         st.best_rec = ri;
@@ -676,8 +678,9 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                                                      int32_t *__restrict__ gbuffer, float *__restrict__ zero_a,
                                                      int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
                                                      const float *__restrict__ verts, const float *__restrict__ cam,
-                                                     int sid)
+                                                     int sid, int tcb)
 {
+    constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     if (!(AB & 16)) {
         // housekeeping spread over all blocks (a few KB each): return fill's bin cursors to zero for
         // the next forward, and zero-fill the caller's gradient accumulators if it passed them
@@ -715,9 +718,9 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const bool in_frame = i < W && j < H;
     const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
 
-    // prefetch the background of this pixel (used if nothing covers it)
+    // prefetch the background of this pixel (used if nothing covers it; hill's is its terrain texture)
     float bgv[CM];
-    if (in_frame) {
+    if (in_frame && !kNoDepth) {
 #pragma unroll
         for (int c = 0; c < CM; ++c)
             if (c < C) bgv[c] = background[o * C + c];
@@ -802,8 +805,9 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                     // R4 without branches (same operation order as sample_depth)
                     const float zw = (R.za * (fxl - R.fx0) + R.zb * (fyl - R.fy0)) + R.z0;
                     const uint32_t q = (uint32_t)(__builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f) * 16777215.0f + 0.5f);
-                    const bool ok = in && zw >= 0.0f && zw <= 1.0f && q < kDepthMax;
-                    const uint64_t key = ((uint64_t)q << 32) | (uint32_t)R.face;
+                    const bool ok = in && zw >= 0.0f && zw <= 1.0f && (kNoDepth || q < kDepthMax);
+                    const uint64_t key = kNoDepth ? (uint64_t)(0xffffffffu - (uint32_t)R.face)
+                                                  : (((uint64_t)q << 32) | (uint32_t)R.face);
                     const bool win = ok && key < st.best;
                     st.best = win ? key : st.best;
                     st.best_rec = win ? (rif & 0x7fffffff) : st.best_rec;
@@ -824,7 +828,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                 int64_t E[3];
                 edge_values(r, i, j, E);
                 if (!inside(r, E)) continue;
-                depth_update(r.za, r.zb, r.fx0, r.fy0, r.z0, r.face, (int32_t)ri, fxl, fyl, st);
+                depth_update<kNoDepth>(r.za, r.zb, r.fx0, r.fy0, r.z0, r.face, (int32_t)ri, fxl, fyl, st);
             }
         }
     }
@@ -839,7 +843,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         gbuffer[o] = -1;
 #pragma unroll
         for (int c2 = 0; c2 < CM; ++c2)
-            if (c2 < C) out[c2] = bgv[c2];
+            if (c2 < C) out[c2] = kNoDepth ? 0.0f : bgv[c2];
         return;
     }
     const Rec &r = frame_recs[st.best_rec];
@@ -867,12 +871,27 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         const ocean::Camera camv{cam[0], cam[1], cam[2], cam[3], cam[4], cam[5], cam[6], cam[7]};
         const float2 col = ocean::shade(tx + sx / (float)W, ty + sy / (float)H, camv, (float)W, (float)H);
         for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 3 ? 1.0f : 0.0f;
-    } else if constexpr (SH == DIRT_SHADER_OCEANIC) {
-        // the oceanic family (shader ids 2..5, `sid` at run time), same texCoordV and jitter as above
+    } else if constexpr (SH == DIRT_SHADER_HILL) {
+        // hill: texCoordV without jitter; the op's background tensor is the terrain lookup (tcb channels)
         const float *vb = verts + (int64_t)b * V * 4;
         const float *p0 = vb + (int64_t)fd.v[0] * 4, *p1 = vb + (int64_t)fd.v[1] * 4, *p2 = vb + (int64_t)fd.v[2] * 4;
         const float tx = (lam[0] * p0[0] + lam[1] * p1[0]) + lam[2] * p2[0];
         const float ty = (lam[0] * p0[1] + lam[1] * p1[1]) + lam[2] * p2[1];
+        const hill::Tex T{background + (int64_t)b * H * W * tcb, H, W, tcb};
+        const float4 col = hill::shade(T, tx, ty, cam);
+        for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 2 ? col.z : k == 3 ? col.w : 0.0f;
+    } else if constexpr (SH == DIRT_SHADER_OCEANIC) {
+        // the oceanic family (shader ids 2..6, `sid` at run time), same texCoordV and jitter as above
+        const float *vb = verts + (int64_t)b * V * 4;
+        const float *p0 = vb + (int64_t)fd.v[0] * 4, *p1 = vb + (int64_t)fd.v[1] * 4, *p2 = vb + (int64_t)fd.v[2] * 4;
+        const float tx = (lam[0] * p0[0] + lam[1] * p1[0]) + lam[2] * p2[0];
+        const float ty = (lam[0] * p0[1] + lam[1] * p1[1]) + lam[2] * p2[1];
+        if (sid == DIRT_SHADER_OCEANIC_OPT_FLOW) {
+            // no jitter (shaders.cpp:1323-1325 commented out); fragColor = (new_coord, 0, 1)
+            const float2 nc = ocean::opt_flow(tx, ty, cam, (float)W, (float)H);
+            for (int k = 0; k < C; ++k) out[k] = k == 0 ? nc.x : k == 1 ? nc.y : k == 3 ? 1.0f : 0.0f;
+            return;
+        }
         const float u = (tx + 1.0f) / 2.0f, v = (ty + 1.0f) / 2.0f;
         int ix = (int)floorf(u * (float)W), iy = (int)floorf(v * (float)H);
         if (!(u * (float)W >= 0.0f)) ix = 0;
@@ -1573,7 +1592,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 3; }
+int dirt_abi_version(void) { return 4; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -1590,21 +1609,27 @@ int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_c
     return DIRT_OK;
 }
 
-int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
-                       const int32_t *faces, const float *camera_pos, int B, int H, int W, int C, int V, int F,
-                       int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch,
-                       size_t scratch_bytes, int64_t bin_capacity, unsigned flags, float *zero_grad_vertices,
-                       float *zero_grad_vertex_colors, void *stream_)
+}  // extern "C"
+
+// the forward of every op; tcb = channels of `background` (== C except for hill's terrain lookup)
+static int rasterise_fwd_impl(const float *background, int tcb, const float *vertices, const float *vertex_colors,
+                              const int32_t *faces, const float *camera_pos, int B, int H, int W, int C, int V, int F,
+                              int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes,
+                              void *scratch, size_t scratch_bytes, int64_t bin_capacity, unsigned flags,
+                              float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream_)
 {
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
-    if (shader_id < DIRT_SHADER_GOURAUD || shader_id > DIRT_SHADER_OCEANIC_SIMPLE_PROXY)
+    if (shader_id < DIRT_SHADER_GOURAUD || shader_id > DIRT_SHADER_HILL)
         return fail(DIRT_EINVAL, "Rasterise: unsupported shader_id");
     if (shader_id != DIRT_SHADER_GOURAUD && !camera_pos)
-        return fail(DIRT_EINVAL, "Rasterise: procedural fragment programs need camera_pos (8 floats, 9 for still_cloud)");
+        return fail(DIRT_EINVAL, "Rasterise: procedural fragment programs need camera_pos");
+    if (shader_id == DIRT_SHADER_HILL && tcb != 1 && tcb != 3 && tcb != 4)
+        return fail(DIRT_EINVAL, "Hill: the terrain lookup must have 1, 3 or 4 channels");
     if (B == 0) return DIRT_OK;
+    const bool need_colors = shader_id == DIRT_SHADER_GOURAUD;
     if (!background || !pixels || !gbuffer || !saved || !scratch || (F > 0 && (!faces || !vertices)) ||
-        (V > 0 && (!vertices || !vertex_colors)))
+        (V > 0 && (!vertices || (need_colors && !vertex_colors))))
         return fail(DIRT_EINVAL, "Rasterise: null tensor pointer");
     Layout L;
     rc = make_layout(B, H, W, F, bin_capacity, L);
@@ -1651,10 +1676,12 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
         background, vertex_colors, recs, fdata, ccursor, coffset, bins, L.bin_capacity, B, H, W, C, V, F, L.ntx,   \
         L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices,                                  \
         zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                      \
-        zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id)
+        zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb)
 #define LAUNCH_RASTER(CC)                                                                                        \
     if (shader_id == DIRT_SHADER_OCEANIC_HORIZON)                                                                \
         LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC_HORIZON);                                                            \
+    else if (shader_id == DIRT_SHADER_HILL)                                                                      \
+        LAUNCH_PROC(CC, DIRT_SHADER_HILL);                                                                       \
     else if (shader_id >= DIRT_SHADER_OCEANIC)                                                                   \
         LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC);                                                                    \
     else                                                                                                         \
@@ -1664,7 +1691,7 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
                                                       zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
                                                       zero_grad_vertex_colors,                                     \
                                                       zero_grad_vertex_colors ? (int64_t)B * V * C : 0,            \
-                                                      vertices, camera_pos, shader_id)
+                                                      vertices, camera_pos, shader_id, tcb)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else LAUNCH_RASTER(0);
@@ -1672,6 +1699,29 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
 #undef LAUNCH_PROC
     HIP_TRY(hipGetLastError());
     return DIRT_OK;
+}
+
+extern "C" {
+
+int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
+                       const int32_t *faces, const float *camera_pos, int B, int H, int W, int C, int V, int F,
+                       int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch,
+                       size_t scratch_bytes, int64_t bin_capacity, unsigned flags, float *zero_grad_vertices,
+                       float *zero_grad_vertex_colors, void *stream_)
+{
+    return rasterise_fwd_impl(background, C, vertices, vertex_colors, faces, camera_pos, B, H, W, C, V, F, shader_id,
+                              pixels, gbuffer, saved, saved_bytes, scratch, scratch_bytes, bin_capacity, flags,
+                              zero_grad_vertices, zero_grad_vertex_colors, stream_);
+}
+
+int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *vertices, const int32_t *faces,
+                  const float *camera_pos, int B, int H, int W, int C, int V, int F, float *pixels, int32_t *gbuffer,
+                  void *saved, size_t saved_bytes, void *scratch, size_t scratch_bytes, int64_t bin_capacity,
+                  void *stream_)
+{
+    return rasterise_fwd_impl(terrain, terrain_channels, vertices, nullptr, faces, camera_pos, B, H, W, C, V, F,
+                              DIRT_SHADER_HILL, pixels, gbuffer, saved, saved_bytes, scratch, scratch_bytes,
+                              bin_capacity, 0u, nullptr, nullptr, stream_);
 }
 
 static NdcScale ndc_scale(int W, int H)
@@ -1749,7 +1799,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
         raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,\
                                                              bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift, \
                                                              L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, 0,  \
-                                                             nullptr, 0, nullptr, nullptr, 0);                      \
+                                                             nullptr, 0, nullptr, nullptr, 0, C);                    \
         break
     switch (variant) {
         V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8);

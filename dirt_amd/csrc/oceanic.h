@@ -449,4 +449,59 @@ __device__ __noinline__ float3 shade_family(const Family P, float xx, float xy, 
     return make_float3(out[0], out[1], out[2]);
 }
 
+// oceanic_opt_flow (shader id 6), shaders.cpp:1178-1398: flat sea (water() = 58), no jitter; cam: 16
+// floats ([9] dt, [10..12] dx,dy,dz, [13..15] dang1..3, oceanic_opt_flow.cpp:399-414).  Returns
+// new_coord; mirrors the oracle's oracle_opt_flow_pixel.
+__device__ __noinline__ float2 opt_flow(float xx, float xy, const float *cam, float width, float height)
+{
+    const float rox = cam[0], roy = cam[1], roz = cam[2], dt = cam[9];
+    float vx = (xx + 1.0f) * width / 2.0f - width / 2.0f;
+    float vy = (xy + 1.0f) * height / 2.0f - height / 2.0f;
+    float vz = 1.73f * width / 2.0f;
+    {
+        const float l = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
+        vx = vx / l; vy = vy / l; vz = vz / l;
+    }
+    float sin1 = sin_fixed(cam[3]), cos1 = cos_fixed(cam[3]);
+    float sin2 = sin_fixed(cam[4]), cos2 = cos_fixed(cam[4]);
+    float sin3 = sin_fixed(cam[5]), cos3 = cos_fixed(cam[5]);
+    const float rx = ((cos2 * cos3) * vx + (-cos1 * sin3 + (sin1 * sin2) * cos3) * vy) +
+                     (sin1 * sin3 + (cos1 * sin2) * cos3) * vz;
+    const float ry = ((cos2 * sin3) * vx + (cos1 * cos3 + (sin1 * sin2) * sin3) * vy) +
+                     (-sin1 * cos3 + (cos1 * sin2) * sin3) * vz;
+    const float rz = (-sin2 * vx + (sin1 * cos2) * vy) + (cos1 * cos2) * vz;
+    sin1 = sin_fixed(cam[3] - cam[13] * dt); cos1 = cos_fixed(cam[3] - cam[13] * dt);
+    sin2 = sin_fixed(cam[4] - cam[14] * dt); cos2 = cos_fixed(cam[4] - cam[14] * dt);
+    sin3 = sin_fixed(cam[5] - cam[15] * dt); cos3 = cos_fixed(cam[5] - cam[15] * dt);
+    float t = -roy / ry;
+    float st = 0.5f, old_h = 0.0f;
+    for (int j = 1000; j < 1020; ++j) {
+        if (t > 500.0f) st = 1.0f;
+        if (t > 800.0f) st = 2.0f;
+        if (t > 1500.0f) st = 3.0f;
+        const float p1 = roy + t * ry;
+        const float h = p1 - 58.0f;
+        t = t + (fmaxf(1.0f, fabsf(h)) * sgn(h)) * st;
+        if (old_h * h < 0.0f) st = st / 2.0f;
+        old_h = h;
+    }
+    float odx = rx, ody = ry, odz = rz;
+    if (!(ry > 0.0f)) {
+        odx = (rox + t * rx) - (rox - cam[10] * dt);
+        ody = (roy + t * ry) - (roy - cam[11] * dt);
+        odz = (roz + t * rz) - (roz - cam[12] * dt);
+    }
+    float ox = ((cos2 * cos3) * odx + (cos2 * sin3) * ody) - sin2 * odz;
+    float oy = ((-cos1 * sin3 + (sin1 * sin2) * cos3) * odx + (cos1 * cos3 + (sin1 * sin2) * sin3) * ody) +
+               (sin1 * cos2) * odz;
+    const float oz = ((sin1 * sin3 + (cos1 * sin2) * cos3) * odx + (-sin1 * cos3 + (cos1 * sin2) * sin3) * ody) +
+                     (cos1 * cos2) * odz;
+    ox = ox / oz;
+    oy = oy / oz;
+    const float s = 1.73f * width / 2.0f;
+    ox = ox * s;
+    oy = oy * s;
+    return make_float2(ox + width / 2.0f, oy + height / 2.0f);
+}
+
 }  // namespace ocean

@@ -108,6 +108,30 @@ def _check_shapes(background, vertices, vertex_colors, faces, H, W, C):
         raise ValueError("Rasterise expects 1 <= channels <= %d" % _lib.MAX_CHANNELS)
 
 
+# floats of camera_pos each program reads (the op's cudaMemcpy of camera_pos to the host)
+_CAMERA_FLOATS = {
+    _lib.SHADER_OCEANIC_STILL_CLOUD: (9, "oceanic_still_cloud needs 9 camera_pos floats: cloud_t is [8] "
+                                         "(csrc/oceanic_still_cloud.cpp:323,407)"),
+    _lib.SHADER_OCEANIC_OPT_FLOW: (16, "oceanic_opt_flow needs 16 camera_pos floats: dt is [9], the camera velocity "
+                                       "[10..15] (csrc/oceanic_opt_flow.cpp:323,399-414)"),
+    _lib.SHADER_HILL: (12, "hill needs 12 camera_pos floats: the camera origin is [9..11] (csrc/hill.cpp:323,395-407)"),
+}
+
+
+def _camera(camera_pos, shader_id, dev):
+    if camera_pos is None:
+        if shader_id != _lib.SHADER_GOURAUD:
+            raise ValueError("procedural fragment programs need camera_pos (8 floats)")
+        return None
+    camera_pos = _as_tensor(camera_pos, torch.float32, dev).contiguous().reshape(-1)
+    if camera_pos.numel() < 8:
+        raise ValueError("camera_pos must hold at least 8 floats (csrc/rasterise_egl.cpp:323)")
+    need, why = _CAMERA_FLOATS.get(shader_id, (8, ""))
+    if camera_pos.numel() < need:
+        raise ValueError(why)
+    return camera_pos
+
+
 def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
                        bin_capacity=0, return_gbuffer=False):
     dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
@@ -115,14 +139,7 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
     vertices = _as_tensor(vertices, torch.float32, dev).contiguous()
     vertex_colors = _as_tensor(vertex_colors, torch.float32, dev).contiguous()
     faces = _as_tensor(faces, torch.int32, dev).contiguous()
-    if camera_pos is not None:
-        camera_pos = _as_tensor(camera_pos, torch.float32, dev).contiguous().reshape(-1)
-        if camera_pos.numel() < 8:
-            raise ValueError("camera_pos must hold at least 8 floats (csrc/rasterise_egl.cpp:323)")
-        if shader_id == _lib.SHADER_OCEANIC_STILL_CLOUD and camera_pos.numel() < 9:
-            raise ValueError("oceanic_still_cloud reads cloud_t from camera_pos[8] (csrc/oceanic_still_cloud.cpp:407)")
-    elif shader_id != _lib.SHADER_GOURAUD:
-        raise ValueError("procedural fragment programs need camera_pos (8 floats)")
+    camera_pos = _camera(camera_pos, shader_id, dev)
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
     pixels, gbuffer = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos,
                                                int(height), int(width), int(channels), shader_id, int(bin_capacity))
@@ -132,7 +149,7 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
 _SHADERS = {None: _lib.SHADER_GOURAUD, "gouraud": _lib.SHADER_GOURAUD,
             "oceanic_horizon": _lib.SHADER_OCEANIC_HORIZON, "oceanic": _lib.SHADER_OCEANIC,
             "oceanic_still_cloud": _lib.SHADER_OCEANIC_STILL_CLOUD, "oceanic_no_cloud": _lib.SHADER_OCEANIC_NO_CLOUD,
-            "oceanic_simple_proxy": _lib.SHADER_OCEANIC_SIMPLE_PROXY}
+            "oceanic_simple_proxy": _lib.SHADER_OCEANIC_SIMPLE_PROXY, "oceanic_opt_flow": _lib.SHADER_OCEANIC_OPT_FLOW}
 
 
 def _shader_id(shader):
@@ -154,14 +171,17 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
         vertex_colors: float32 [vertex count, channels]; interpolated perspective-correctly (Gouraud)
         faces: int32 [face count, 3] indices into `vertices`
         camera_pos: float32 [>=8] (cam x, y, z, ang1, ang2, ang3, time, light_z,
-            csrc/rasterise_egl.cpp:399-406); read only by the `oceanic_horizon` program
+            csrc/rasterise_egl.cpp:399-406; 9 floats for oceanic_still_cloud, 16 for oceanic_opt_flow);
+            read only by the procedural programs
         height, width, channels: may be None, then inferred from `background`'s shape
         name: ignored (TensorFlow name scope in the reference)
         shader: fragment program. None / 'gouraud': Gouraud colours (upstream DIRT, the default);
             'oceanic_horizon': the program the fork's `Rasterise` op binds (csrc/shaders.cpp:1668-1919,
             rasterise_egl.cpp:385): covered pixels get (sky mask, sun / reflection, 0), jittered by the
             background's first two channels; needs camera_pos and has no gradient (the reference
-            registers none)
+            registers none).  'oceanic', 'oceanic_still_cloud', 'oceanic_no_cloud',
+            'oceanic_simple_proxy', 'oceanic_opt_flow': the programs of the reference's other procedural
+            ops (same as calling those ops); forward only
 
     Returns:
         float32 [height, width, channels] pixels, differentiable w.r.t. background, vertices, vertex_colors.
@@ -213,14 +233,48 @@ def _procedural_op(opname, shader, ref):
     return op
 
 
-def _not_yet(opname):
-    def op(background, vertices, vertex_colors, faces, camera_pos, height=None, width=None, channels=None,
-           name=None):
-        raise NotImplementedError(
-            "%s: procedural fragment program not implemented yet on MI355X (SURVEY 8f-4)" % opname)
-    op.__name__ = opname
-    op.__doc__ = "Reference dirt/rasterise_ops.py procedural op `%s` (SURVEY 8f-4), not built yet." % opname
-    return op
+def hill(background, vertices, vertex_colors, faces, camera_pos, height=None, width=None, channels=None, name=None):
+    """Reference dirt/rasterise_ops.py:186-203 `hill` (op csrc/hill.cpp, program csrc/shaders.cpp:123-554).
+
+    `background` is the terrain lookup [height, width, 1|3|4] (x = terrain height, yzw = normal): the op
+    checks only its height and width (hill.cpp:310).  `vertex_colors` is shape-checked and not read;
+    camera_pos holds 12 floats, of which [9..11] (the camera origin) are read.  There is no depth test:
+    where faces overlap the last one in draw order wins (hill.cpp:194); uncovered pixels are 0.
+    Forward only, like the reference.  Returns float32 [height, width, channels].
+    """
+    del name
+    bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
+    if height is None:
+        height = int(bshape[0])
+    if width is None:
+        width = int(bshape[1])
+    if channels is None:
+        channels = int(bshape[2])
+    dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
+    terrain = _as_tensor(background, torch.float32, dev).contiguous()[None]
+    vertices = _as_tensor(vertices, torch.float32, dev).contiguous()[None]
+    vertex_colors = _as_tensor(vertex_colors, torch.float32, dev).contiguous()[None]
+    faces = _as_tensor(faces, torch.int32, dev).contiguous()[None]
+    camera_pos = _camera(camera_pos, _lib.SHADER_HILL, dev)
+    H, W, C = int(height), int(width), int(channels)
+    if terrain.dim() != 4 or tuple(terrain.shape[1:3]) != (H, W):
+        raise ValueError("Rasterise expects background_tensor to be 4D, and bgcolor.shape == [None, height, width, channels]")
+    if terrain.shape[3] not in (1, 3, 4):
+        raise ValueError("hill: the terrain lookup (background) must have 1, 3 or 4 channels (csrc/rasterise_egl.cu:33-47)")
+    _check_shapes(terrain.new_empty((terrain.shape[0], H, W, C)), vertices, vertex_colors, faces, H, W, C)
+    B, V, F = vertices.shape[0], vertices.shape[1], faces.shape[1]
+    lib = _lib.load()
+    saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, 0)
+    pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+    gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+    saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
+    scratch = torch.empty((max(scratch_bytes, 1),), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.dirt_hill_fwd(terrain.data_ptr(), int(terrain.shape[3]), vertices.data_ptr(), faces.data_ptr(),
+                                     camera_pos.data_ptr(), B, H, W, C, V, F, pixels.data_ptr(), gbuffer.data_ptr(),
+                                     saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, 0, stream))
+    return pixels[0]
 
 
 # RasteriseGrad binds the `oceanic` program (csrc/rasterise_grad_egl.cpp:399, SURVEY F4: not a gradient)
@@ -228,5 +282,4 @@ rasterise_grad = _procedural_op("rasterise_grad", "oceanic", "rasterise_ops.py:9
 oceanic_no_cloud = _procedural_op("oceanic_no_cloud", "oceanic_no_cloud", "rasterise_ops.py:110-127")
 oceanic_simple_proxy = _procedural_op("oceanic_simple_proxy", "oceanic_simple_proxy", "rasterise_ops.py:129-146")
 oceanic_still_cloud = _procedural_op("oceanic_still_cloud", "oceanic_still_cloud", "rasterise_ops.py:148-165")
-oceanic_opt_flow = _not_yet("oceanic_opt_flow")
-hill = _not_yet("hill")
+oceanic_opt_flow = _procedural_op("oceanic_opt_flow", "oceanic_opt_flow", "rasterise_ops.py:167-184")

@@ -11,6 +11,10 @@
  *                                 never defined in the fork) -- the gradient DIRT registers upstream
  *                                 for "Rasterise"; the fork's REGISTER_OP("RasteriseGrad")
  *                                 (csrc/rasterise_grad_egl.cpp:33-53) is a forward render
+ *   dirt_hill_fwd       replaces  REGISTER_OP("Hill") + HillOpGpu     csrc/hill.cpp:33-53, 282-498
+ *                                 (the other procedural ops are shader ids of dirt_rasterise_fwd:
+ *                                 RasteriseGrad, OceanicStillCloud, OceanicNoCloud, OceanicOptFlow,
+ *                                 OceanicSimpleProxy -- csrc/rasterise_grad_egl.cpp, csrc/oceanic_*.cpp)
  *   dirt_last_error     replaces  OP_REQUIRES(..., errors::InvalidArgument(...)) messages,
  *                                 csrc/rasterise_egl.cpp:310-336 (the reference aborts on everything
  *                                 else via LOG(FATAL)/CHECK; this ABI never aborts)
@@ -57,8 +61,12 @@ extern "C" {
 #define DIRT_SHADER_OCEANIC_STILL_CLOUD 3 /* csrc/shaders.cpp:866-1176 (`OceanicStillCloud`; camera_pos[8] = cloud_t) */
 #define DIRT_SHADER_OCEANIC_NO_CLOUD 4    /* csrc/shaders.cpp:1402-1666 (`OceanicNoCloud`) */
 #define DIRT_SHADER_OCEANIC_SIMPLE_PROXY 5 /* csrc/shaders.cpp:1921-2185 (`OceanicSimpleProxy`) */
+#define DIRT_SHADER_OCEANIC_OPT_FLOW 6 /* csrc/shaders.cpp:1178-1398 (`OceanicOptFlow`; camera_pos: 16 floats,
+                                          oceanic_opt_flow.cpp:399-414); pixels = previous-frame coordinates */
+#define DIRT_SHADER_HILL 7 /* csrc/shaders.cpp:123-554 (`Hill`, csrc/hill.cpp; camera_pos: 12 floats); no depth
+                              test (last face wins), background = terrain lookup, uncovered pixels 0 */
 
-/* ABI version, bumped on any signature change */
+/* ABI version, bumped on any signature change (4: + dirt_hill_fwd, shader ids 6 and 7) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -69,8 +77,10 @@ int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_c
 /* Forward: pixels = Rasterise(background, vertices, vertex_colors, faces).
  * gbuffer [B,H,W] int32 receives the per-pixel visible setup-record index (-1 = background),
  * which together with `saved` is what dirt_rasterise_bwd consumes.
- * camera_pos: device pointer to >= 8 floats (9 for DIRT_SHADER_OCEANIC_STILL_CLOUD), used only by the
- * procedural programs (shader_id != 0; may be NULL for Gouraud). */
+ * camera_pos: device pointer to >= 8 floats (9 for DIRT_SHADER_OCEANIC_STILL_CLOUD, 16 for
+ * DIRT_SHADER_OCEANIC_OPT_FLOW, 12 for DIRT_SHADER_HILL), used only by the procedural programs
+ * (shader_id != 0; may be NULL for Gouraud).  DIRT_SHADER_HILL here reads `background` as a C-channel
+ * terrain lookup; dirt_hill_fwd takes one with its own channel count. */
 int dirt_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
                        const int32_t *faces, const float *camera_pos,
                        int B, int H, int W, int C, int V, int F, int shader_id,
@@ -78,6 +88,14 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
                        void *saved, size_t saved_bytes, void *scratch, size_t scratch_bytes,
                        int64_t bin_capacity, unsigned flags,
                        float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream);
+/* Forward of the Hill op (csrc/hill.cpp:282-498, REGISTER_OP("Hill") :33-53): DIRT_SHADER_HILL with a
+ * terrain lookup `terrain` [B,H,W,terrain_channels] (1, 3 or 4 channels, uploaded like a background,
+ * rasterise_egl.cu:33-47) in place of the background; vertex colours are not read.  pixels [B,H,W,C];
+ * gbuffer / saved / scratch as dirt_rasterise_fwd (same dirt_workspace_sizes). */
+int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *vertices, const int32_t *faces,
+                  const float *camera_pos, int B, int H, int W, int C, int V, int F,
+                  float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch,
+                  size_t scratch_bytes, int64_t bin_capacity, void *stream);
 /* flags of dirt_rasterise_fwd.  Every forward returns the scratch's bin counters to zero when it
  * completes, so a scratch buffer that was zero-filled once (or passed to dirt_scratch_clear) and since
  * used only by forwards with the same B, H, W, F and bin_capacity is "clean". */

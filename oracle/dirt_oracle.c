@@ -239,6 +239,14 @@ static inline int sample_depth(const orc_rec *r, int i, int j, uint32_t *d)
     return 1;
 }
 
+/* R4 without the depth comparison (hill: GL_DEPTH_TEST off): inside the near/far range */
+static inline int sample_in_range(const orc_rec *r, int i, int j)
+{
+    float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
+    float zw = (r->za * (fx - r->fx0) + r->zb * (fy - r->fy0)) + r->z0;
+    return zw >= 0.0f && zw <= 1.0f;
+}
+
 /* R6: perspective-correct parent barycentrics from (possibly doubled) edge values */
 static inline int parent_lambda(const orc_rec *r, const int64_t E[3], float lam[3])
 {
@@ -791,9 +799,349 @@ void oracle_oceanic_family_pixel(int shader_id, const float *bgframe, int H, int
     ocn_family_shade(P, tx + sx / (float)W, ty + sy / (float)H, cam, (float)W, (float)H, out);
 }
 
+/* ------------------------------------------------------------------------------------------------ */
+/* oceanic_opt_flow (shader id 6), shaders.cpp:1178-1398, op csrc/oceanic_opt_flow.cpp.  Optical flow
+ * of a flat sea: water() is the constant waterlevel - 12 = 58 (:1283-1286), no jitter (:1323-1325 are
+ * commented out).  camera_pos (oceanic_opt_flow.cpp:399-414): [0..7] as the family, [9] dt, [10..12]
+ * dx,dy,dz, [13..15] dang1..3 ([8] is not read).  Writes new_coord = the pixel position of the same
+ * world point in the previous frame (:1376-1395; fragColor.xy, z = 0, w = 1). */
+void oracle_opt_flow_pixel(float xyx, float xyy, const float *cam, float width, float height, float out[2])
+{
+    const float ro[3] = {cam[0], cam[1], cam[2]};
+    const float dt = cam[9];
+    float rdv[3];
+    rdv[0] = (xyx + 1.0f) * width / 2.0f - width / 2.0f;
+    rdv[1] = (xyy + 1.0f) * height / 2.0f - height / 2.0f;
+    rdv[2] = 1.73f * width / 2.0f;
+    ocn_normalize(rdv);
+    float sin1 = ocn_sin(cam[3]), cos1 = ocn_cos(cam[3]);
+    float sin2 = ocn_sin(cam[4]), cos2 = ocn_cos(cam[4]);
+    float sin3 = ocn_sin(cam[5]), cos3 = ocn_cos(cam[5]);
+    float rd[3];
+    rd[0] = ((cos2 * cos3) * rdv[0] + (-cos1 * sin3 + (sin1 * sin2) * cos3) * rdv[1]) +
+            (sin1 * sin3 + (cos1 * sin2) * cos3) * rdv[2];
+    rd[1] = ((cos2 * sin3) * rdv[0] + (cos1 * cos3 + (sin1 * sin2) * sin3) * rdv[1]) +
+            (-sin1 * cos3 + (cos1 * sin2) * sin3) * rdv[2];
+    rd[2] = (-sin2 * rdv[0] + (sin1 * cos2) * rdv[1]) + (cos1 * cos2) * rdv[2];
+    /* the previous frame's angles (:1337-1342) */
+    sin1 = ocn_sin(cam[3] - cam[13] * dt); cos1 = ocn_cos(cam[3] - cam[13] * dt);
+    sin2 = ocn_sin(cam[4] - cam[14] * dt); cos2 = ocn_cos(cam[4] - cam[14] * dt);
+    sin3 = ocn_sin(cam[5] - cam[15] * dt); cos3 = ocn_cos(cam[5] - cam[15] * dt);
+    /* trace(), :1288-1321, against the constant water height */
+    float t = -ro[1] / rd[1];
+    float st = 0.5f, old_h = 0.0f;
+    for (int j = 1000; j < 1020; ++j) {
+        if (t > 500.0f) st = 1.0f;
+        if (t > 800.0f) st = 2.0f;
+        if (t > 1500.0f) st = 3.0f;
+        const float p1 = ro[1] + t * rd[1];
+        const float h = p1 - 58.0f;
+        t = t + (fmaxf(1.0f, fabsf(h)) * ocn_sign(h)) * st;
+        if (old_h * h < 0.0f) st = st / 2.0f;
+        old_h = h;
+    }
+    float od[3];
+    if (rd[1] > 0.0f) {
+        od[0] = rd[0]; od[1] = rd[1]; od[2] = rd[2];
+    } else {
+        const float dv[3] = {cam[10], cam[11], cam[12]};
+        for (int k = 0; k < 3; ++k) {
+            const float wpos = ro[k] + t * rd[k];
+            const float old_cam = ro[k] - dv[k] * dt;
+            od[k] = wpos - old_cam;
+        }
+    }
+    /* inverse rotation at the previous angles, projection (:1376-1393) */
+    float ox = ((cos2 * cos3) * od[0] + (cos2 * sin3) * od[1]) - sin2 * od[2];
+    float oy = ((-cos1 * sin3 + (sin1 * sin2) * cos3) * od[0] + (cos1 * cos3 + (sin1 * sin2) * sin3) * od[1]) +
+               (sin1 * cos2) * od[2];
+    const float oz = ((sin1 * sin3 + (cos1 * sin2) * cos3) * od[0] + (-sin1 * cos3 + (cos1 * sin2) * sin3) * od[1]) +
+                     (cos1 * cos2) * od[2];
+    ox = ox / oz;
+    oy = oy / oz;
+    const float s = 1.73f * width / 2.0f;
+    ox = ox * s;
+    oy = oy * s;
+    out[0] = ox + width / 2.0f;
+    out[1] = oy + height / 2.0f;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* hill (shader id 7), shaders.cpp:123-554, op csrc/hill.cpp.  David Hoskins' "rolling hills" over a
+ * terrain lookup texture: the background tensor (any of 1/3/4 channels, hill.cpp:310 does not check the
+ * channel count) uploaded like every background (rasterise_egl.cu:16-47: rows flipped, C=1 broadcast,
+ * alpha 1 for C<4) into a GL_LINEAR / CLAMP_TO_EDGE texture (hill.cpp:232-236); .x = terrain height,
+ * .yzw = normal.  camera_pos: 12 floats (hill.cpp:395-407); r00..r22 are shadowed by main()'s local
+ * constants (shaders.cpp:473-481), so only o0,o1,o2 = [9],[10],[11] are read.  Same float32 rules as the
+ * oceanic programs; additionally: texture() = bilinear in float32 at texel centres (i+0.5)/W, with
+ * weights a = x - floor(x) (the driver's fixed-point filter weights are not emulated); pow(x, 2.0) with a
+ * possibly negative x (DoLighting) = x*x; uninitialised old_h in Scene() = 0. */
+typedef struct {
+    const float *tex; /* one frame, [H][W][C], rows top-first */
+    int H, W, C;
+} hill_tex;
+
+static void hill_texel(const hill_tex *T, int i, int j, int nch, float out[4])
+{
+    i = i < 0 ? 0 : (i > T->W - 1 ? T->W - 1 : i);
+    j = j < 0 ? 0 : (j > T->H - 1 ? T->H - 1 : j);
+    const float *p = T->tex + ((int64_t)(T->H - 1 - j) * T->W + i) * T->C;
+    out[0] = p[0];
+    if (nch == 1) return;
+    if (T->C == 1) { out[1] = p[0]; out[2] = p[0]; out[3] = 1.0f; }
+    else if (T->C == 3) { out[1] = p[1]; out[2] = p[2]; out[3] = 1.0f; }
+    else { out[1] = p[1]; out[2] = p[2]; out[3] = p[3]; }
+}
+
+/* texture(TerrainLookup, (u,v)) for u,v in [0,1]; nch = 1 (.x only) or 4 */
+static void hill_sample(const hill_tex *T, float u, float v, int nch, float out[4])
+{
+    const float x = u * (float)T->W - 0.5f, y = v * (float)T->H - 0.5f;
+    const float fx = floorf(x), fy = floorf(y);
+    const float a = x - fx, b = y - fy;
+    const int i0 = (int)fx, j0 = (int)fy;
+    float t00[4], t10[4], t01[4], t11[4];
+    hill_texel(T, i0, j0, nch, t00);
+    hill_texel(T, i0 + 1, j0, nch, t10);
+    hill_texel(T, i0, j0 + 1, nch, t01);
+    hill_texel(T, i0 + 1, j0 + 1, nch, t11);
+    for (int k = 0; k < nch; ++k) {
+        const float r0 = t00[k] * (1.0f - a) + t10[k] * a;
+        const float r1 = t01[k] * (1.0f - a) + t11[k] * a;
+        out[k] = r0 * (1.0f - b) + r1 * b;
+    }
+}
+
+/* Terrain(p.xz).x (:219-227): texture coordinate clamp(scaled_p.yx, 0, 1) */
+static float hill_terrain(const hill_tex *T, float px, float pz)
+{
+    const float sx = (px - -14.0f) / 28.0f, sz = (pz - 5.0f) / 20.0f;
+    float t[4];
+    hill_sample(T, ocn_clamp01(sz), ocn_clamp01(sx), 1, t);
+    return t[0] * 10.3f - 6.1f;
+}
+
+/* Terrain_normal(p.xz) (:229-237) */
+static void hill_terrain_normal(const hill_tex *T, float px, float pz, float n[3])
+{
+    const float sx = (px - -14.0f) / 28.0f, sz = (pz - 5.0f) / 20.0f;
+    float t[4];
+    hill_sample(T, ocn_clamp01(sz), ocn_clamp01(sx), 4, t);
+    n[0] = t[1] * 2.0f - 1.0f; n[1] = t[2] * 2.0f - 1.0f; n[2] = t[3] * 2.0f - 1.0f;
+}
+
+/* Hash(float) / Hash(vec2), MOD2 = (3.07965, 7.4235) (:160-175) */
+static float hill_hash1(float p)
+{
+    float x = ocn_fract(p / 3.07965f), y = ocn_fract(p / 7.4235f);
+    const float d = y * (x + 19.19f) + x * (y + 19.19f);
+    x = x + d; y = y + d;
+    return ocn_fract(x * y);
+}
+static float hill_hash2(float px, float py)
+{
+    float x = ocn_fract(px / 3.07965f), y = ocn_fract(py / 7.4235f);
+    const float d = x * (y + 19.19f) + y * (x + 19.19f);
+    x = x + d; y = y + d;
+    return ocn_fract(x * y);
+}
+
+/* Noise(vec2) (:179-189) */
+static float hill_noise(float x, float y)
+{
+    const float px = floorf(x), py = floorf(y);
+    float fx = ocn_fract(x), fy = ocn_fract(y);
+    fx = (fx * fx) * (3.0f - 2.0f * fx);
+    fy = (fy * fy) * (3.0f - 2.0f * fy);
+    const float n = px + py * 57.0f;
+    return ocn_mix(ocn_mix(hill_hash1(n + 0.0f), hill_hash1(n + 1.0f), fx),
+                   ocn_mix(hill_hash1(n + 57.0f), hill_hash1(n + 58.0f), fx), fy);
+}
+
+/* Voronoi (:191-209); returns (max(.4 - sqrt(res), 0), id) */
+static void hill_voronoi(float x, float y, float out[2])
+{
+    const float px = floorf(x), py = floorf(y);
+    const float fx = ocn_fract(x), fy = ocn_fract(y);
+    float res = 100.0f, id = 0.0f;
+    for (int j = -1; j <= 1; ++j)
+        for (int i = -1; i <= 1; ++i) {
+            const float bx = (float)i, by = (float)j;
+            const float h = hill_hash2(px + bx, py + by);
+            const float rx = (bx - fx) + h, ry = (by - fy) + h;
+            const float d = rx * rx + ry * ry;
+            if (d < res) {
+                res = d;
+                id = h;
+            }
+        }
+    out[0] = fmaxf(0.4f - sqrtf(res), 0.0f);
+    out[1] = id;
+}
+
+/* DE(p) (:287-300), iTime = 0 */
+static void hill_de(const hill_tex *T, float px, float py, float pz, float out[3])
+{
+    const float iTime = 0.0f;
+    const float base = hill_terrain(T, px, pz) - 1.3f;
+    const float qx = px * 4.0f, qz = pz * 4.0f;
+    const float height = (hill_noise(qx * 2.0f, qz * 2.0f) * 0.75f + hill_noise(qx, qz) * 0.35f) +
+                         hill_noise(qx * 0.5f, qz * 0.5f) * 0.2f;
+    float y = (py - base) - height;
+    y = y * y;
+    const float s0 = ocn_sin(y * 4.0f + qz * 12.3f), s1 = ocn_sin(y * 4.0f + qx * 12.3f);
+    const float w0 = ocn_sin(iTime * 2.3f + 1.5f * qz), w1 = ocn_sin(iTime * 3.6f + 1.5f * qx);
+    const float ax = (qx * 2.5f + s0 * 0.12f) + (w0 * y) * 0.5f;
+    const float ay = (qz * 2.5f + s1 * 0.12f) + (w1 * y) * 0.5f;
+    float v[2];
+    hill_voronoi(ax, ay, v);
+    const float f = v[0] * 0.6f + y * 0.58f;
+    out[0] = y - f * 1.4f;
+    out[1] = ocn_clamp01(f * 1.5f);
+    out[2] = v[1];
+}
+
+/* GetSky (:254-263) */
+static void hill_sky(const float rd[3], const float sun[3], float out[3])
+{
+    const float sunc[3] = {1.0f, 0.75f, 0.6f};
+    const float lo[3] = {0.1f, 0.2f, 0.3f};
+    const float sunAmount = fmaxf(ocn_dot3(rd, sun), 0.0f);
+    const float v = ocn_pow_pos(1.0f - fmaxf(rd[1], 0.0f), 6.0f);
+    const float p800 = fminf(ocn_pow_pos(sunAmount, 800.0f) * 1.5f, 0.3f);
+    for (int k = 0; k < 3; ++k) {
+        float s = ocn_mix(lo[k], 0.32f, v);
+        s = s + ((sunc[k] * sunAmount) * sunAmount) * 0.25f;
+        s = s + sunc[k] * p800;
+        out[k] = ocn_clamp01(s);
+    }
+}
+
+/* Scene (:393-428); returns hit, *resT */
+static int hill_scene(const hill_tex *T, const float ro[3], const float rd[3], float *resT)
+{
+    float t = -(ro[1] + 1.0f) / rd[1];
+    float t_inc = 0.0f;
+    if (rd[1] > -0.015f) t = 80.0f;
+    float h = 0.0f, st = 1.0f, old_h = 0.0f;
+    for (int j = 0; j < 100; ++j) {
+        t = t + t_inc;
+        const float p0 = ro[0] + t * rd[0], p1 = ro[1] + t * rd[1], p2 = ro[2] + t * rd[2];
+        h = p1 - hill_terrain(T, p0, p2);
+        t_inc = (fmaxf(1.0f, fabsf(h)) * ocn_sign(h)) * st;
+        if (h * old_h < 0.0f) st = st / 2.0f;
+        old_h = h;
+    }
+    *resT = t;
+    return fabsf(h) < 0.05f;
+}
+
+/* main() (:453-551) at texCoordV (tx, ty); writes fragColor (4 floats) */
+void oracle_hill_pixel(const float *tex_frame, int H, int W, int Ct, float tx, float ty, const float *cam,
+                       float out[4])
+{
+    const hill_tex T = {tex_frame, H, W, Ct};
+    const float width = (float)W, height = (float)H;
+    const float xyx = (tx + 1.0f) / 2.0f, xyy = (ty * -1.0f + 1.0f) / 2.0f;
+    if (fabsf(xyy * height - height / 2.0f) / (width / 2.0f) >= 0.5625f) {
+        out[0] = out[1] = out[2] = out[3] = 0.0f;
+        return;
+    }
+    float sun[3] = {0.35f, 0.2f, 0.3f};
+    ocn_normalize(sun);
+    float rv[3] = {xyx * width - width / 2.0f, xyy * height - height / 2.0f, 0.85f * width};
+    ocn_normalize(rv);
+    const float ro[3] = {-cam[9], cam[11], cam[10]};
+    const float r00 = 0.999999573f, r01 = -0.0000933038802f, r02 = 0.000919791287f;
+    const float r10 = 0.000918443273f, r11 = -0.0135434586f, r12 = -0.999907861f;
+    const float r20 = 0.000105752439f, r21 = 0.999908279f, r22 = -0.0135433672f;
+    float dir[3];
+    dir[0] = -((r00 * rv[0] + r10 * rv[1]) + r20 * rv[2]);
+    dir[2] = (r01 * rv[0] + r11 * rv[1]) + r21 * rv[2];
+    dir[1] = (r02 * rv[0] + r12 * rv[1]) + r22 * rv[2];
+    float col[3], dist;
+    if (!hill_scene(&T, ro, dir, &dist)) {
+        hill_sky(dir, sun, col);
+    } else {
+        const float pos[3] = {ro[0] + dist * dir[0], ro[1] + dist * dir[1], ro[2] + dist * dir[2]};
+        float nor[3];
+        hill_terrain_normal(&T, pos[0], pos[2], nor);
+        /* TerrainColour (:363-377), type 0 */
+        float mat[3];
+        const float nz = hill_noise(pos[0] * 0.025f, pos[2] * 0.025f);
+        const float m0[3] = {0.0f, 0.3f, 0.0f}, m1[3] = {0.2f, 0.3f, 0.0f};
+        for (int k = 0; k < 3; ++k) mat[k] = ocn_mix(m0[k], m1[k], nz);
+        float fn = 0.0f, w = 0.7f, nx = pos[0] * 0.1f, ny = pos[2] * 0.1f; /* FractalNoise (:242-252) */
+        for (int i = 0; i < 3; ++i) {
+            fn = fn + hill_noise(nx, ny) * w;
+            w = w * 0.6f;
+            nx = 2.0f * nx;
+            ny = 2.0f * ny;
+        }
+        const float tsh = fn + 0.5f;
+        /* GrassBlades (:317-346) */
+        {
+            const float rCoC = fmaxf((dist * 0.3f) * 0.04f, (2.0f / height) * (1.0f + dist * 0.3f));
+            float d = 0.0f, alpha = 0.0f;
+            float cw[4] = {mat[0] * 0.15f, mat[1] * 0.15f, mat[2] * 0.15f, 0.0f};
+            for (int i = 0; i < 15; ++i) {
+                if (cw[3] > 0.99f) break;
+                float ret[3];
+                hill_de(&T, pos[0] + dir[0] * d, pos[1] + dir[1] * d, pos[2] + dir[2] * d, ret);
+                ret[0] = ret[0] + 0.5f * rCoC;
+                if (ret[0] < rCoC) {
+                    alpha = (1.0f - cw[1]) * ocn_clamp01((-ret[0] - -rCoC) / (rCoC - -rCoC));
+                    const float tip[3] = {0.35f, 0.35f, fminf(ocn_pow_pos(ret[2], 4.0f) * 35.0f, 0.35f)};
+                    const float wt = ocn_pow_pos(ret[1], 9.0f) * 0.7f;
+                    for (int k = 0; k < 3; ++k) {
+                        const float gra = ocn_mix(mat[k], tip[k], wt) * ret[1];
+                        cw[k] = cw[k] + gra * alpha;
+                    }
+                    cw[3] = cw[3] + alpha;
+                }
+                d = d + fmaxf(ret[0] * 0.7f, 0.1f);
+            }
+            if (cw[3] < 0.2f) { cw[0] = 0.1f; cw[1] = 0.15f; cw[2] = 0.05f; }
+            for (int k = 0; k < 3; ++k) mat[k] = cw[k] * tsh;
+        }
+        /* DoLighting (:351-356) */
+        const float sl = ocn_dot3(sun, nor);
+        const float hl = (sl * sl) * 4.0f;
+        const float sunc[3] = {1.0f, 0.75f, 0.6f};
+        for (int k = 0; k < 3; ++k) mat[k] = (mat[k] * sunc[k]) * hl;
+        /* ApplyFog (:267-271) */
+        const float fog = ocn_clamp01((dist * dist) * 0.0000012f);
+        float sky[3];
+        hill_sky(dir, sun, sky);
+        for (int k = 0; k < 3; ++k) col[k] = ocn_mix(mat[k], sky[k], fog);
+    }
+    /* PostEffects (:437-451) */
+    float rgb[3];
+    for (int k = 0; k < 3; ++k) rgb[k] = ocn_pow_pos(col[k], 0.45f) * 1.3f;
+    const float lum = (0.2125f * rgb[0] + 0.7154f * rgb[1]) + 0.0721f * rgb[2];
+    const float vig = 0.4f + 0.5f * ocn_pow_pos((((40.0f * xyx) * xyy) * (1.0f - xyx)) * (1.0f - xyy), 0.2f);
+    for (int k = 0; k < 3; ++k) out[k] = ocn_mix(0.5f, ocn_mix(lum, rgb[k], 1.3f), 1.1f) * vig;
+    out[3] = 1.0f;
+}
+
+static int fwd_core(const float *background, int Cb, const float *vertices, const float *vertex_colors,
+                    const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
+                    const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads);
+
 int oracle_rasterise_fwd_shader(const float *background, const float *vertices, const float *vertex_colors,
                                 const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
-                                const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads);
+                                const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
+{
+    return fwd_core(background, C, vertices, vertex_colors, faces, B, H, W, C, V, F, shader_id, camera_pos, pixels,
+                    gbuffer, nthreads);
+}
+
+/* the Hill op (csrc/hill.cpp): terrain lookup [B,H,W,Ct] (Ct in {1,3,4}) in place of the background */
+int oracle_hill_fwd(const float *terrain, int Ct, const float *vertices, const int32_t *faces, int B, int H, int W,
+                    int C, int V, int F, const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
+{
+    return fwd_core(terrain, Ct, vertices, NULL, faces, B, H, W, C, V, F, 7, camera_pos, pixels, gbuffer, nthreads);
+}
 
 int oracle_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
                          const int32_t *faces, int B, int H, int W, int C, int V, int F,
@@ -803,10 +1151,13 @@ int oracle_rasterise_fwd(const float *background, const float *vertices, const f
                                        pixels, gbuffer, nthreads);
 }
 
-/* shader_id 0 = Gouraud, 1 = oceanic_horizon (camera_pos: 8 host floats, rasterise_egl.cpp:399-406) */
-int oracle_rasterise_fwd_shader(const float *background, const float *vertices, const float *vertex_colors,
-                                const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
-                                const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
+/* shader_id (include/dirt_mi355x.h): 0 Gouraud, 1 oceanic_horizon, 2..5 the oceanic family,
+ * 6 oceanic_opt_flow, 7 hill (no depth test: the last face in draw order wins, hill.cpp:194;
+ * uncovered pixels 0, hill never writes its colour attachment there); camera_pos: host floats.
+ * background has Cb channels (Cb == C except for hill's terrain lookup). */
+static int fwd_core(const float *background, int Cb, const float *vertices, const float *vertex_colors,
+                    const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
+                    const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
 {
     int status = 0;
 #ifdef _OPENMP
@@ -819,7 +1170,7 @@ int oracle_rasterise_fwd_shader(const float *background, const float *vertices, 
     int32_t *rbuf = (int32_t *)malloc(sizeof(int32_t) * (size_t)H * W);
     for (int b = 0; b < B; ++b) {
         const float *vb = vertices + (int64_t)b * V * 4;
-        const float *cb = vertex_colors + (int64_t)b * V * C;
+        const float *cb = vertex_colors ? vertex_colors + (int64_t)b * V * C : NULL;
         const int32_t *fb = faces + (int64_t)b * F * 3;
         if (setup_frame(vb, fb, V, F, W, H, recs, nsub, clipped)) status = 2;
         /* raster: parallel over bands of window rows; key-min is order independent */
@@ -839,9 +1190,16 @@ int oracle_rasterise_fwd_shader(const float *background, const float *vertices, 
                             int64_t E[3];
                             edge_values(r, i, j, E);
                             if (!inside(r, E)) continue;
-                            uint32_t d;
-                            if (!sample_depth(r, i, j, &d)) continue;
-                            uint64_t key = ((uint64_t)d << 32) | (uint32_t)f;
+                            uint64_t key;
+                            if (shader_id == 7) {
+                                /* depth test off; near/far clipping still applies (zw in [0,1]) */
+                                if (!sample_in_range(r, i, j)) continue;
+                                key = (uint64_t)(0xffffffffu - (uint32_t)f);
+                            } else {
+                                uint32_t d;
+                                if (!sample_depth(r, i, j, &d)) continue;
+                                key = ((uint64_t)d << 32) | (uint32_t)f;
+                            }
                             int64_t p = (int64_t)j * W + i;
                             if (key < keys[p]) { keys[p] = key; rbuf[p] = (int32_t)ri; }
                         }
@@ -854,11 +1212,11 @@ int oracle_rasterise_fwd_shader(const float *background, const float *vertices, 
                     int64_t p = (int64_t)j * W + i;
                     int64_t o = (((int64_t)b * H + row) * W + i);
                     float *out = pixels + o * C;
-                    const float *bg = background + o * C;
+                    const float *bg = background + o * Cb;
                     int32_t ri = rbuf[p];
                     if (gbuffer) gbuffer[o] = ri < 0 ? -1 : (ri | (clipped[recs[ri].face] ? GBUF_MULTI : 0));
                     if (ri < 0) {
-                        for (int c = 0; c < C; ++c) out[c] = bg[c];
+                        for (int c = 0; c < C; ++c) out[c] = shader_id == 7 ? 0.0f : bg[c];
                         continue;
                     }
                     const orc_rec *r = &recs[ri];
@@ -867,6 +1225,22 @@ int oracle_rasterise_fwd_shader(const float *background, const float *vertices, 
                     float lam[3] = {0.0f, 0.0f, 0.0f};
                     parent_lambda(r, E, lam);
                     const int32_t *f3 = fb + 3 * (int64_t)r->face;
+                    if (shader_id == 6 || shader_id == 7) {
+                        const float tx = (lam[0] * vb[(int64_t)f3[0] * 4] + lam[1] * vb[(int64_t)f3[1] * 4]) +
+                                         lam[2] * vb[(int64_t)f3[2] * 4];
+                        const float ty = (lam[0] * vb[(int64_t)f3[0] * 4 + 1] + lam[1] * vb[(int64_t)f3[1] * 4 + 1]) +
+                                         lam[2] * vb[(int64_t)f3[2] * 4 + 1];
+                        float col[4];
+                        if (shader_id == 6) {
+                            oracle_opt_flow_pixel(tx, ty, camera_pos, (float)W, (float)H, col);
+                            col[2] = 0.0f;
+                            col[3] = 1.0f;
+                        } else {
+                            oracle_hill_pixel(background + (int64_t)b * H * W * Cb, H, W, Cb, tx, ty, camera_pos, col);
+                        }
+                        for (int c = 0; c < C; ++c) out[c] = c < 4 ? col[c] : 0.0f;
+                        continue;
+                    }
                     if (shader_id >= 2) {
                         const float tx = (lam[0] * vb[(int64_t)f3[0] * 4] + lam[1] * vb[(int64_t)f3[1] * 4]) +
                                          lam[2] * vb[(int64_t)f3[2] * 4];

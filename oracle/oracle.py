@@ -34,6 +34,12 @@ def load():
         lib.oracle_oceanic_horizon_pixel.restype = None
         lib.oracle_oceanic_family_pixel.argtypes = [I, P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
         lib.oracle_oceanic_family_pixel.restype = None
+        lib.oracle_opt_flow_pixel.argtypes = [ctypes.c_float, ctypes.c_float, P, ctypes.c_float, ctypes.c_float, P]
+        lib.oracle_opt_flow_pixel.restype = None
+        lib.oracle_hill_pixel.argtypes = [P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
+        lib.oracle_hill_pixel.restype = None
+        lib.oracle_hill_fwd.argtypes = [P, I, P, P, I, I, I, I, I, I, P, P, P, I]
+        lib.oracle_hill_fwd.restype = I
         lib.oracle_rasterise_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, I]
         lib.oracle_rasterise_bwd.restype = I
         lib.oracle_max_threads.argtypes = []
@@ -54,9 +60,53 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+CAMERA_FLOATS = {3: 9, 6: 16, 7: 12}
+
+
+def hill_fwd(terrain, vertices, faces, channels, camera_pos, nthreads=0):
+    """The Hill op: terrain [B,H,W,Ct] (Ct in 1/3/4), vertices [B,V,4], faces [B,F,3], camera_pos (12
+    floats).  Returns (pixels [B,H,W,channels], gbuffer, status)."""
+    tr, vs, fs = _f32(terrain), _f32(vertices), _i32(faces)
+    B, H, W, Ct = tr.shape
+    V, F = vs.shape[1], fs.shape[1]
+    pixels = np.empty((B, H, W, channels), np.float32)
+    gbuf = np.empty((B, H, W), np.int32)
+    cam = np.zeros(16, np.float32)
+    c = _f32(camera_pos).reshape(-1)
+    if c.size < 12:
+        raise ValueError("hill needs camera_pos (12 floats)")
+    cam[:min(c.size, 16)] = c[:16]
+    st = load().oracle_hill_fwd(_ptr(tr), Ct, _ptr(vs), _ptr(fs), B, H, W, channels, V, F, _ptr(cam), _ptr(pixels),
+                                _ptr(gbuf), nthreads)
+    return pixels, gbuf, st
+
+
+def opt_flow_pixel(tx, ty, camera_pos, width, height):
+    """oceanic_opt_flow's fragment program alone at texCoordV = (tx, ty): returns new_coord (2 floats)."""
+    out = np.zeros(2, np.float32)
+    cam = np.zeros(16, np.float32)
+    c = _f32(camera_pos).reshape(-1)
+    cam[:min(c.size, 16)] = c[:16]
+    load().oracle_opt_flow_pixel(float(tx), float(ty), _ptr(cam), float(width), float(height), _ptr(out))
+    return out
+
+
+def hill_pixel(terrain_frame, tx, ty, camera_pos):
+    """hill's fragment program alone at texCoordV = (tx, ty) over a [H,W,Ct] terrain: returns fragColor."""
+    tr = _f32(terrain_frame)
+    H, W, Ct = tr.shape
+    out = np.zeros(4, np.float32)
+    cam = np.zeros(16, np.float32)
+    c = _f32(camera_pos).reshape(-1)
+    cam[:min(c.size, 16)] = c[:16]
+    load().oracle_hill_pixel(_ptr(tr), H, W, Ct, float(tx), float(ty), _ptr(cam), _ptr(out))
+    return out
+
+
 def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0, shader_id=0, camera_pos=None):
     """Batched forward.  background [B,H,W,C], vertices [B,V,4], vertex_colors [B,V,C], faces [B,F,3].
-    shader_id 0 = Gouraud, 1 = oceanic_horizon (camera_pos: 8 floats).
+    shader_id 0 = Gouraud, 1 = oceanic_horizon, 2..5 the oceanic family, 6 oceanic_opt_flow (camera_pos:
+    8 floats; 9 for oceanic_still_cloud, 16 for oceanic_opt_flow).
 
     Returns (pixels [B,H,W,C] float32, gbuffer [B,H,W] int32 record index or -1, status)."""
     bg, vs, cs, fs = _f32(background), _f32(vertices), _f32(vertex_colors), _i32(faces)
@@ -67,9 +117,9 @@ def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0, shader
     cam = np.zeros(16, np.float32)
     if camera_pos is not None:
         c = _f32(camera_pos).reshape(-1)
-        cam[:c.size] = c
-        if shader_id >= 1 and c.size < (9 if shader_id == 3 else 8):
-            raise ValueError("procedural programs need camera_pos (8 floats, 9 for oceanic_still_cloud)")
+        cam[:min(c.size, 16)] = c[:16]
+        if shader_id >= 1 and c.size < CAMERA_FLOATS.get(shader_id, 8):
+            raise ValueError("procedural programs need camera_pos (%d floats)" % CAMERA_FLOATS.get(shader_id, 8))
     st = load().oracle_rasterise_fwd_shader(_ptr(bg), _ptr(vs), _ptr(cs), _ptr(fs), B, H, W, C, V, F, shader_id,
                                             _ptr(cam), _ptr(pixels), _ptr(gbuf), nthreads)
     return pixels, gbuf, st

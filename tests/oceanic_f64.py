@@ -273,3 +273,216 @@ def render_family_fullscreen(sid, H, W, cam):
     ty = (j + 0.5) / H * 2.0 - 1.0
     out, rd = shade_family(sid, tx.ravel(), ty.ravel(), cam, float(W), float(H))
     return np.moveaxis(out.reshape(3, H, W), 0, -1)[::-1], rd[1].reshape(H, W)[::-1]
+
+
+# ---- oceanic_opt_flow (shaders.cpp:1178-1398), float64 --------------------------------------------------
+def _rot(cam3, cam4, cam5):
+    s1, c1, s2, c2, s3, c3 = np.sin(cam3), np.cos(cam3), np.sin(cam4), np.cos(cam4), np.sin(cam5), np.cos(cam5)
+    # rows: ray_dir_p = R @ ray_dir (shaders.cpp:1330-1333)
+    return np.array([[c2 * c3, -c1 * s3 + s1 * s2 * c3, s1 * s3 + c1 * s2 * c3],
+                     [c2 * s3, c1 * c3 + s1 * s2 * s3, -s1 * c3 + c1 * s2 * s3],
+                     [-s2, s1 * c2, c1 * c2]])
+
+
+def opt_flow(tx, ty, cam, width, height):
+    """new_coord for arrays of texCoordV (no jitter); cam: 16 floats (oceanic_opt_flow.cpp:399-414)."""
+    cam = np.asarray(cam, np.float64)
+    dt = cam[9]
+    rdv = np.stack([(tx + 1.0) * width / 2.0 - width / 2.0, (ty + 1.0) * height / 2.0 - height / 2.0,
+                    np.full_like(tx, 1.73 * width / 2.0)])
+    rdv = rdv / np.sqrt((rdv * rdv).sum(0))
+    rd = _rot(cam[3], cam[4], cam[5]) @ rdv
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = -cam[1] / rd[1]
+    st = np.full_like(t, 0.5)
+    old_h = np.zeros_like(t)
+    for _ in range(20):
+        st = np.where(t > 500.0, 1.0, st)
+        st = np.where(t > 800.0, 2.0, st)
+        st = np.where(t > 1500.0, 3.0, st)
+        h = cam[1] + t * rd[1] - 58.0
+        t = t + np.maximum(1.0, np.abs(h)) * np.sign(h) * st
+        st = np.where(old_h * h < 0.0, st / 2.0, st)
+        old_h = h
+    wpos = cam[:3, None] + t * rd
+    old_rd = np.where(rd[1] > 0.0, rd, wpos - (cam[:3] - cam[10:13] * dt)[:, None])
+    o = _rot(cam[3] - cam[13] * dt, cam[4] - cam[14] * dt, cam[5] - cam[15] * dt).T @ old_rd
+    o = o / o[2] * (1.73 * width / 2.0)
+    return o[0] + width / 2.0, o[1] + height / 2.0, rd
+
+
+def render_opt_flow_fullscreen(H, W, cam):
+    j = np.arange(H, dtype=np.float64)[:, None] * np.ones((1, W))
+    i = np.arange(W, dtype=np.float64)[None, :] * np.ones((H, 1))
+    tx = (i + 0.5) / W * 2.0 - 1.0
+    ty = (j + 0.5) / H * 2.0 - 1.0
+    x, y, rd = opt_flow(tx.ravel(), ty.ravel(), cam, float(W), float(H))
+    return np.stack([x.reshape(H, W), y.reshape(H, W)], -1)[::-1], rd[1].reshape(H, W)[::-1]
+
+
+# ---- hill (shaders.cpp:123-554), float64 ---------------------------------------------------------------
+def _hill_sample(T, u, v, ch):
+    """GL_LINEAR / CLAMP_TO_EDGE lookup of channel(s) ch of a [H, W, 4] texel array (GL rows bottom first)."""
+    H, W = T.shape[:2]
+    x, y = u * W - 0.5, v * H - 0.5
+    fx, fy = np.floor(x), np.floor(y)
+    a, b = (x - fx)[..., None], (y - fy)[..., None]
+    i0, j0 = fx.astype(np.int64), fy.astype(np.int64)
+
+    def tx(i, j):
+        return T[np.clip(j, 0, H - 1), np.clip(i, 0, W - 1)][..., ch]
+    r0 = tx(i0, j0) * (1 - a) + tx(i0 + 1, j0) * a
+    r1 = tx(i0, j0 + 1) * (1 - a) + tx(i0 + 1, j0 + 1) * a
+    return r0 * (1 - b) + r1 * b
+
+
+def _hill_uv(px, pz):
+    return np.clip((pz - 5.0) / 20.0, 0, 1), np.clip((px + 14.0) / 28.0, 0, 1)
+
+
+def _hill_terrain(T, px, pz):
+    u, v = _hill_uv(px, pz)
+    return _hill_sample(T, u, v, [0])[..., 0] * 10.3 - 6.1
+
+
+def _hill_hash1(p):
+    x, y = _fract(p / 3.07965), _fract(p / 7.4235)
+    d = y * (x + 19.19) + x * (y + 19.19)
+    return _fract((x + d) * (y + d))
+
+
+def _hill_hash2(px, py):
+    x, y = _fract(px / 3.07965), _fract(py / 7.4235)
+    d = x * (y + 19.19) + y * (x + 19.19)
+    return _fract((x + d) * (y + d))
+
+
+def _hill_noise(x, y):
+    px, py = np.floor(x), np.floor(y)
+    fx, fy = _fract(x), _fract(y)
+    fx, fy = fx * fx * (3 - 2 * fx), fy * fy * (3 - 2 * fy)
+    n = px + py * 57.0
+    return _mix(_mix(_hill_hash1(n), _hill_hash1(n + 1), fx), _mix(_hill_hash1(n + 57), _hill_hash1(n + 58), fx), fy)
+
+
+def _hill_voronoi(x, y):
+    px, py = np.floor(x), np.floor(y)
+    fx, fy = _fract(x), _fract(y)
+    res, idv = np.full_like(x, 100.0), np.zeros_like(x)
+    for j in (-1, 0, 1):
+        for i in (-1, 0, 1):
+            h = _hill_hash2(px + i, py + j)
+            d = (i - fx + h) ** 2 + (j - fy + h) ** 2
+            better = d < res
+            res, idv = np.where(better, d, res), np.where(better, h, idv)
+    return np.maximum(0.4 - np.sqrt(res), 0.0), idv
+
+
+def _hill_de(T, px, py, pz):
+    base = _hill_terrain(T, px, pz) - 1.3
+    qx, qz = px * 4.0, pz * 4.0
+    height = _hill_noise(qx * 2, qz * 2) * 0.75 + _hill_noise(qx, qz) * 0.35 + _hill_noise(qx * 0.5, qz * 0.5) * 0.2
+    y = (py - base - height) ** 2
+    ax = qx * 2.5 + np.sin(y * 4.0 + qz * 12.3) * 0.12 + np.sin(1.5 * qz) * y * 0.5
+    ay = qz * 2.5 + np.sin(y * 4.0 + qx * 12.3) * 0.12 + np.sin(1.5 * qx) * y * 0.5
+    vx, vid = _hill_voronoi(ax, ay)
+    f = vx * 0.6 + y * 0.58
+    return y - f * 1.4, np.clip(f * 1.5, 0, 1), vid
+
+
+def _hill_sky(rd, sun):
+    amt = np.maximum((rd * sun[:, None]).sum(0), 0.0)
+    v = (1.0 - np.maximum(rd[1], 0.0)) ** 6.0
+    sunc = np.array([1.0, 0.75, 0.6])[:, None]
+    sky = _mix(np.array([0.1, 0.2, 0.3])[:, None], 0.32, v) + sunc * amt * amt * 0.25
+    sky = sky + sunc * np.minimum(amt ** 800.0 * 1.5, 0.3)
+    return np.clip(sky, 0, 1)
+
+
+def hill(tex, tx, ty, cam):
+    """fragColor [4, n] for arrays of texCoordV over a terrain lookup [H, W, Ct] (rows top first)."""
+    with np.errstate(all="ignore"):  # far grass samples overflow (y*y), as in float32
+        return _hill(tex, tx, ty, cam)
+
+
+def _hill(tex, tx, ty, cam):
+    tex = np.asarray(tex, np.float64)
+    H, W, Ct = tex.shape
+    T = np.ones((H, W, 4))
+    if Ct == 1:
+        T[..., :3] = tex[..., :1]
+    else:
+        T[..., :Ct] = tex
+    T = T[::-1]  # GL rows bottom first
+    width, height = float(W), float(H)
+    cam = np.asarray(cam, np.float64)
+    xyx, xyy = (tx + 1) / 2, (-ty + 1) / 2
+    box = np.abs(xyy * height - height / 2) / (width / 2) >= 0.5625
+    sun = np.array([0.35, 0.2, 0.3])
+    sun = sun / np.sqrt(sun @ sun)
+    rv = np.stack([xyx * width - width / 2, xyy * height - height / 2, np.full_like(xyx, 0.85 * width)])
+    rv = rv / np.sqrt((rv * rv).sum(0))
+    R = np.array([[0.999999573, -0.0000933038802, 0.000919791287], [0.000918443273, -0.0135434586, -0.999907861],
+                  [0.000105752439, 0.999908279, -0.0135433672]])  # [r_row][col]
+    d = np.stack([-(R[0, 0] * rv[0] + R[1, 0] * rv[1] + R[2, 0] * rv[2]),
+                  R[0, 2] * rv[0] + R[1, 2] * rv[1] + R[2, 2] * rv[2],
+                  R[0, 1] * rv[0] + R[1, 1] * rv[1] + R[2, 1] * rv[2]])
+    ro = np.array([-cam[9], cam[11], cam[10]])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = -(ro[1] + 1.0) / d[1]
+    t = np.where(d[1] > -0.015, 80.0, t)
+    t_inc, st, old_h, h = np.zeros_like(t), np.ones_like(t), np.zeros_like(t), np.zeros_like(t)
+    for _ in range(100):
+        t = t + t_inc
+        p = ro[:, None] + t * d
+        h = p[1] - _hill_terrain(T, p[0], p[2])
+        t_inc = np.maximum(1.0, np.abs(h)) * np.sign(h) * st
+        st = np.where(h * old_h < 0, st / 2, st)
+        old_h = h
+    hit = np.abs(h) < 0.05
+    dist = t
+    sky = _hill_sky(d, sun)
+    pos = ro[:, None] + dist * d
+    u, v = _hill_uv(pos[0], pos[2])
+    nor = (_hill_sample(T, u, v, [1, 2, 3]) * 2 - 1).T
+    nz = _hill_noise(pos[0] * 0.025, pos[2] * 0.025)
+    mat = _mix(np.array([0.0, 0.3, 0.0])[:, None], np.array([0.2, 0.3, 0.0])[:, None], nz)
+    fn, w, nx, ny = 0.0, 0.7, pos[0] * 0.1, pos[2] * 0.1
+    for _ in range(3):
+        fn, w, nx, ny = fn + _hill_noise(nx, ny) * w, w * 0.6, 2 * nx, 2 * ny
+    rcoc = np.maximum(dist * 0.3 * 0.04, (2.0 / height) * (1.0 + dist * 0.3))
+    cw = np.concatenate([mat * 0.15, np.zeros_like(mat[:1])])
+    dd = np.zeros_like(dist)
+    live = np.ones_like(dist, bool)
+    for _ in range(15):
+        live = live & ~(cw[3] > 0.99)
+        rx, ry, rz = _hill_de(T, pos[0] + d[0] * dd, pos[1] + d[1] * dd, pos[2] + d[2] * dd)
+        rx = rx + 0.5 * rcoc
+        take = live & (rx < rcoc)
+        alpha = (1 - cw[1]) * np.clip((-rx + rcoc) / (2 * rcoc), 0, 1)
+        tip = np.stack([np.full_like(rz, 0.35), np.full_like(rz, 0.35), np.minimum(rz ** 4 * 35, 0.35)])
+        gra = _mix(mat, tip, ry ** 9.0 * 0.7) * ry
+        cw = np.where(take, cw + np.concatenate([gra * alpha, alpha[None]]), cw)
+        dd = np.where(live, dd + np.maximum(rx * 0.7, 0.1), dd)
+    cw[:3] = np.where(cw[3] < 0.2, np.array([0.1, 0.15, 0.05])[:, None], cw[:3])
+    mat = cw[:3] * (fn + 0.5)
+    hl = ((sun[:, None] * nor).sum(0)) ** 2 * 4
+    mat = mat * np.array([1.0, 0.75, 0.6])[:, None] * hl
+    fog = np.clip(dist * dist * 0.0000012, 0, 1)
+    col = np.where(hit, _mix(mat, sky, fog), sky)
+    rgb = np.maximum(col, 0) ** 0.45 * 1.3
+    lum = 0.2125 * rgb[0] + 0.7154 * rgb[1] + 0.0721 * rgb[2]
+    vig = 0.4 + 0.5 * np.maximum(40 * xyx * xyy * (1 - xyx) * (1 - xyy), 0) ** 0.2
+    out = _mix(0.5, _mix(lum, rgb, 1.3), 1.1) * vig
+    out = np.concatenate([out, np.ones_like(out[:1])])
+    return np.where(box, 0.0, out), hit & ~box, box
+
+
+def render_hill_fullscreen(tex, cam):
+    H, W = np.asarray(tex).shape[:2]
+    j = np.arange(H, dtype=np.float64)[:, None] * np.ones((1, W))
+    i = np.arange(W, dtype=np.float64)[None, :] * np.ones((H, 1))
+    tx = (i + 0.5) / W * 2.0 - 1.0
+    ty = (j + 0.5) / H * 2.0 - 1.0
+    out, hit, box = hill(tex, tx.ravel(), ty.ravel(), cam)
+    return (np.moveaxis(out.reshape(4, H, W), 0, -1)[::-1], hit.reshape(H, W)[::-1], box.reshape(H, W)[::-1])

@@ -208,3 +208,22 @@ def deferred_mesh_scene(W=512, H=512, C=7, n=100, seed=0):
     attrs = np.concatenate([normals, albedo, depth], 1)[:, :C].astype(np.float32)
     bg = np.zeros((H, W, C), np.float32)
     return bg, clip, attrs, faces
+
+
+def hill_terrain(H, W, C=4):
+    """Synthetic terrain lookup for the `hill` program (x = height in [0, 1], yzw = normal * 0.5 + 0.5,
+    the layout shaders.cpp:219-237 decodes); rows top first like any background."""
+    y, x = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    h = 0.5 + 0.25 * np.sin(6.1 * x + 1.3) * np.cos(4.7 * y) + 0.15 * np.sin(13 * x * y + 0.4)
+    gy, gx = np.gradient(h)
+    n = np.stack([-gx * 40, np.ones_like(h), -gy * 40], -1)
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    t = np.concatenate([h[..., None], (n + 1) / 2], -1).astype(np.float32)
+    return t[..., :C].copy() if C != 4 else t
+
+
+def fullscreen_quad():
+    """The procedural ops' harness geometry (tests/square_test.py:16,31): two faces covering the frame."""
+    v = np.array([[-1, -1, 0, 1], [-1, 1, 0, 1], [1, 1, 0, 1], [1, -1, 0, 1]], np.float32)
+    f = np.array([[0, 1, 2], [0, 2, 3]], np.int32)
+    return v, f

@@ -51,9 +51,23 @@ def test_shape_validation_messages(shapes, msg):
             rasterise_ops._check_shapes(*ts, 8, 8, 3)
 
 
-def test_procedural_ops_not_yet_available():
-    with pytest.raises(NotImplementedError):
-        dirt_amd.hill(None, None, None, None, None)
+def test_camera_pos_lengths_per_program():
+    # floats each op copies to the host: 8 (rasterise_egl.cpp:323), 9 (oceanic_still_cloud.cpp:323),
+    # 16 (oceanic_opt_flow.cpp:323), 12 (hill.cpp:323)
+    from dirt_amd import _lib
+    cpu = torch.device("cpu")
+    for sid, n in ((_lib.SHADER_OCEANIC_HORIZON, 8), (_lib.SHADER_OCEANIC_STILL_CLOUD, 9),
+                   (_lib.SHADER_OCEANIC_OPT_FLOW, 16), (_lib.SHADER_HILL, 12)):
+        assert rasterise_ops._camera(np.zeros(n), sid, cpu).numel() == n
+        with pytest.raises(ValueError):
+            rasterise_ops._camera(np.zeros(n - 1), sid, cpu)
+    with pytest.raises(ValueError, match="camera_pos"):
+        rasterise_ops._camera(None, _lib.SHADER_HILL, cpu)
+    assert rasterise_ops._camera(None, _lib.SHADER_GOURAUD, cpu) is None
+    assert rasterise_ops._shader_id("oceanic_opt_flow") == 6
+    params = list(inspect.signature(dirt_amd.hill).parameters)
+    assert params == ["background", "vertices", "vertex_colors", "faces", "camera_pos", "height", "width",
+                      "channels", "name"]
 
 
 def test_matrices_match_reference_formulas():

@@ -112,3 +112,100 @@ def test_procedural_op_names():
         ref, _, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None], shader_id=sid,
                                          camera_pos=np.array(cam, np.float32))
         np.testing.assert_array_equal(px.cpu().numpy(), ref[0])
+
+
+# ---- oceanic_opt_flow (shader id 6) and hill (shader id 7, dirt_hill_fwd) -------------------------------
+from test_procedural_oracle import FLOW_CAMS, HILL_CAMS, hill_cam  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(FLOW_CAMS))
+def test_opt_flow_bit_exact(name):
+    cam = FLOW_CAMS[name]
+    for C in (1, 3, 4):
+        px, gb = _family_fwd(6, *fullscreen(96, 128, C=C), cam=cam)
+        rpx, rgb, _ = oracle.rasterise_fwd(*fullscreen(96, 128, C=C), shader_id=6, camera_pos=np.array(cam, np.float32))
+        np.testing.assert_array_equal(gb, rgb)
+        np.testing.assert_array_equal(px, rpx)
+
+
+def test_opt_flow_mesh_and_public_op():
+    import dirt_amd
+    bg, v, c, f = scenes.random_triangles(F=300, W=120, H=80, C=3, radius_px=16.0, seed=8, perspective=True)
+    cam = FLOW_CAMS["rotate"]
+    px = dirt_amd.oceanic_opt_flow(torch.from_numpy(bg).cuda(), torch.from_numpy(v).cuda(), torch.from_numpy(c).cuda(),
+                                   torch.from_numpy(f).cuda(), torch.tensor(cam).cuda())
+    ref, _, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None], shader_id=6,
+                                     camera_pos=np.array(cam, np.float32))
+    np.testing.assert_array_equal(px.cpu().numpy(), ref[0])
+    with pytest.raises(ValueError, match="16"):
+        dirt_amd.oceanic_opt_flow(torch.from_numpy(bg).cuda(), torch.from_numpy(v).cuda(), torch.from_numpy(c).cuda(),
+                                  torch.from_numpy(f).cuda(), torch.zeros(15).cuda())
+
+
+def _hill_gpu(T, v, f, C, cam):
+    from dirt_amd import _lib
+    B, H, W, Ct = T.shape
+    V, F = v.shape[1], f.shape[1]
+    lib = _lib.load()
+    saved_b, scratch_b = _lib.workspace_sizes(B, H, W, C, V, F, 0)
+    t, vv, ff, cc = (torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (T, v, f, cam))
+    px = torch.empty((B, H, W, C), dtype=torch.float32, device="cuda")
+    gb = torch.empty((B, H, W), dtype=torch.int32, device="cuda")
+    saved = torch.empty(max(saved_b, 1), dtype=torch.uint8, device="cuda")
+    scratch = torch.empty(max(scratch_b, 1), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.dirt_hill_fwd(t.data_ptr(), Ct, vv.data_ptr(), ff.data_ptr(), cc.data_ptr(), B, H, W, C, V, F,
+                                 px.data_ptr(), gb.data_ptr(), saved.data_ptr(), saved_b, scratch.data_ptr(), scratch_b,
+                                 0, torch.cuda.current_stream().cuda_stream))
+    return px.cpu().numpy(), gb.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", sorted(HILL_CAMS))
+def test_hill_bit_exact(name):
+    v, f = scenes.fullscreen_quad()
+    cam = hill_cam(HILL_CAMS[name])
+    for (H, W) in ((54, 96), (64, 64)):
+        for Ct, C in ((4, 3), (1, 1), (3, 4)):
+            T = scenes.hill_terrain(H, W, Ct)[None]
+            px, gb = _hill_gpu(T, v[None], f[None], C, cam)
+            rpx, rgb, _ = oracle.hill_fwd(T, v[None], f[None], C, cam)
+            np.testing.assert_array_equal(gb, rgb)
+            np.testing.assert_array_equal(px, rpx)
+
+
+def test_hill_harness_960x540_and_public_op():
+    """tests/square_test.py:14-37: full-screen square, 960x540, channels=3, a 4-channel terrain lookup."""
+    import dirt_amd
+    v, f = scenes.fullscreen_quad()
+    T = scenes.hill_terrain(540, 960, 4)
+    cam = hill_cam(HILL_CAMS["harness"])
+    px = dirt_amd.hill(torch.from_numpy(T).cuda(), torch.from_numpy(v).cuda(), torch.ones(4, 3).cuda(),
+                       torch.from_numpy(f).cuda(), torch.from_numpy(cam).cuda(), height=540, width=960, channels=3)
+    ref, _, _ = oracle.hill_fwd(T[None], v[None], f[None], 3, cam)
+    np.testing.assert_array_equal(px.cpu().numpy(), ref[0])
+    with pytest.raises(ValueError, match="12"):
+        dirt_amd.hill(torch.from_numpy(T).cuda(), torch.from_numpy(v).cuda(), torch.ones(4, 3).cuda(),
+                      torch.from_numpy(f).cuda(), torch.zeros(11).cuda(), channels=3)
+    with pytest.raises(ValueError, match="1, 3 or 4"):
+        dirt_amd.hill(torch.zeros(540, 960, 2).cuda(), torch.from_numpy(v).cuda(), torch.ones(4, 3).cuda(),
+                      torch.from_numpy(f).cuda(), torch.from_numpy(cam).cuda(), channels=3)
+
+
+def test_hill_overlap_and_mesh():
+    """No depth test (last face wins) and uncovered pixels 0, on overlapping quads and a random mesh."""
+    H, W = 32, 48
+    T = scenes.hill_terrain(H, W, 4)[None]
+    near = [[-0.5, -0.5, -0.5, 1], [-0.5, 0.5, -0.5, 1], [0.5, 0.5, -0.5, 1], [0.5, -0.5, -0.5, 1]]
+    far = [[-0.8, -0.8, 0.5, 1], [-0.8, 0.8, 0.5, 1], [0.8, 0.8, 0.5, 1], [0.8, -0.8, 0.5, 1]]
+    v = np.array([near + far], np.float32)
+    f = np.array([[[0, 1, 2], [0, 2, 3], [4, 5, 6], [4, 6, 7]]], np.int32)
+    cam = hill_cam(HILL_CAMS["harness"])
+    px, gb = _hill_gpu(T, v, f, 3, cam)
+    rpx, rgb, _ = oracle.hill_fwd(T, v, f, 3, cam)
+    np.testing.assert_array_equal(gb, rgb)
+    np.testing.assert_array_equal(px, rpx)
+    _, v, _, f = scenes.random_triangles(F=400, W=96, H=64, C=3, radius_px=18.0, seed=12, perspective=True)
+    T = scenes.hill_terrain(64, 96, 4)[None]
+    px, gb = _hill_gpu(T, v[None], f[None], 3, cam)
+    rpx, rgb, _ = oracle.hill_fwd(T, v[None], f[None], 3, cam)
+    np.testing.assert_array_equal(gb, rgb)
+    np.testing.assert_array_equal(px, rpx)
