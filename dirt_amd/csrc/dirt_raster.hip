@@ -5,9 +5,11 @@
 //
 //   K1 setup_kernel    one thread per (frame, face): fetch 3 clip vertices, project + snap (R1/R2),
 //                      edge equations (R3), depth plane (R4), guard-band clipping (R5, rare slow path);
-//                      writes 128-B setup records + 32-B FaceData, counts (tile, triangle) bin entries.
-//   K2 scan_kernel     exclusive scan of per-tile counts.
-//   K3 fill_kernel     scatter each record index into the bins of the 16x16 tiles its bbox overlaps.
+//                      writes 128-B setup records + 32-B FaceData, counts (coarse tile, record) pairs
+//                      (one fire-and-forget device atomic per touched (workgroup, coarse tile)).
+//   K3 fill_kernel     every workgroup scans its frame's per-tile totals into bin offsets (frame-local
+//                      bin regions), then scatters each record index into the coarse bins it overlaps.
+//                      (K2, a separate scan launch, no longer exists; its profile slot stays empty.)
 //   K4 raster_kernel   one 256-thread workgroup per 16x16 tile (a wave per 16x4 strip): stages the
 //                      tile's records in LDS with strip-relative 32-bit edge values (exact), each lane
 //                      owns one pixel and keeps the min (depth24<<32 | face) key, then resolves
@@ -100,8 +102,9 @@ struct Layout {
     int nctx, ncty, ncoarse;  // coarse tiles per frame (<= kMaxCoarse)
     int64_t nrec;
     size_t saved_recs, saved_fdata, saved_total;
-    size_t off_count, off_cursor, off_done, off_offset, off_flag, off_bins, scratch_total;
+    size_t off_count, off_cursor, off_offset, off_flag, off_bins, scratch_total;
     int64_t bin_capacity;
+    int64_t frame_capacity;   // bins of frame b: [b * frame_capacity, (b + 1) * frame_capacity)
 };
 
 constexpr int kMaxCoarse = 4096;   // LDS histogram size in setup/fill
@@ -135,10 +138,10 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.saved_total = L.saved_fdata + (size_t)align_up((int64_t)B * F * (int64_t)sizeof(FaceData), 256);
     const int64_t nc = (int64_t)B * L.ncoarse;
     size_t o = 0;
+    L.frame_capacity = B > 0 ? L.bin_capacity / B : 0;
     L.off_count = o;  o += (size_t)align_up(nc * 4, 256);
     L.off_cursor = o; o += (size_t)align_up(nc * 4, 256);
-    L.off_done = o;   o += 256;  // setup's finished-block ticket (zeroed with the counts)
-    L.off_offset = o; o += (size_t)align_up((nc + 1) * 8, 256);
+    L.off_offset = o; o += (size_t)align_up((nc + B) * 8, 256);  // ncoarse + 1 offsets per frame
     L.off_flag = o;   o += 256;
     L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 8, 256);
     L.scratch_total = o;
@@ -299,73 +302,11 @@ __device__ __forceinline__ void coarse_pairs_flush(BigQueue &Q, Op op)
     __syncthreads();
 }
 
-constexpr int kScanThreads = 1024;
-constexpr int kScanPerThread = 4;
-
-// exclusive prefix sum of the bin counts (uint32) into bin offsets (uint64) by one workgroup of NT
-// threads; counts are read with agent-scope atomic loads (they were produced by other workgroups'
-// atomics in the same launch when called from setup_kernel)
-template <int NT>
-__device__ void scan_counts(const uint32_t *in, uint64_t *__restrict__ out, int64_t n)
-{
-    __shared__ uint64_t wave_sums[NT / 64];
-    __shared__ uint64_t carry_s;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint64_t carry = 0;
-    for (int64_t base = 0; base < n; base += (int64_t)NT * kScanPerThread) {
-        const int64_t k0 = base + (int64_t)t * kScanPerThread;
-        uint32_t v[kScanPerThread];
-        uint64_t local = 0;
-#pragma unroll
-        for (int q = 0; q < kScanPerThread; ++q)
-            v[q] = (k0 + q < n) ? __hip_atomic_load(in + k0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-        for (int q = 0; q < kScanPerThread; ++q) local += v[q];
-        uint64_t x = local;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) wave_sums[wave] = x;
-        __syncthreads();
-        if (wave == 0) {
-            uint64_t w = lane < NT / 64 ? wave_sums[lane] : 0;
-#pragma unroll
-            for (int d = 1; d < NT / 64; d <<= 1) {
-                const uint64_t y = __shfl_up(w, d, 64);
-                if (lane >= d) w += y;
-            }
-            if (lane < NT / 64) wave_sums[lane] = w;
-            if (lane == NT / 64 - 1) carry_s = w;
-        }
-        __syncthreads();
-        uint64_t run = carry + (wave > 0 ? wave_sums[wave - 1] : 0) + (x - local);
-#pragma unroll
-        for (int q = 0; q < kScanPerThread; ++q) {
-            if (k0 + q < n) out[k0 + q] = run;
-            run += v[q];
-        }
-        carry += carry_s;
-        __syncthreads();
-    }
-    if (t == 0) out[n] = carry;  // n + 1 offsets: bin k holds [out[k], out[k+1])
-}
-
-// stand-alone scan (frames without faces: setup_kernel is not launched)
-__global__ __launch_bounds__(kScanThreads) void scan_kernel(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                            int64_t n)
-{
-    scan_counts<kScanThreads>(in, out, n);
-}
-
 __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restrict__ verts,
                                                             const int32_t *__restrict__ faces, int V, int F, int W,
                                                             int H, int cshift, int nctx, int ncoarse, int64_t nrec,
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
-                                                            uint32_t *__restrict__ ccount, uint32_t *__restrict__ flag,
-                                                            uint32_t *__restrict__ done, uint64_t *__restrict__ coffset,
-                                                            int64_t nc)
+                                                            uint32_t *__restrict__ ccount, uint32_t *__restrict__ flag)
 {
     __shared__ uint32_t hist[kMaxCoarse];
     __shared__ BigQueue Q;
@@ -438,27 +379,13 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         fdata[gid] = fd;
     }
     coarse_pairs_flush<kBinThreads>(Q, count);
+    // one device atomic per touched (workgroup, coarse tile), without return: nothing in this launch
+    // waits for them (a device-scope round trip costs ~2 us); fill reads the totals after the launch
+    // boundary and scans them itself
     uint32_t *cc = ccount + (int64_t)b * ncoarse;
-    // count atomics WITH return: a returned value means the add has been performed at the coherence
-    // point, so after the barrier this block's counts are all in before its ticket (no release fence,
-    // which would write back the whole L2)
-    uint32_t sink = 0;
     for (int c = t; c < ncoarse; c += kBinThreads)
-        if (hist[c]) sink |= atomicAdd(&cc[c], hist[c]);
-    __shared__ uint32_t s_ticket;
-    if (sink == 0xffffffffu) s_ticket = 0;  // consume the returns (never true in practice)
-    __syncthreads();
-    // the last block to take a ticket turns the counts into bin offsets (saves a dependent scan
-    // launch); it reads the counts with agent-scope atomic loads
-    if (t == 0) s_ticket = atomicAdd(done, 1u);
-    __syncthreads();
-    if (s_ticket != gridDim.x * gridDim.y - 1) return;
-    scan_counts<kBinThreads>(ccount, coffset, nc);
+        if (hist[c]) __hip_atomic_fetch_add(&cc[c], hist[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-// ------------------------------------------------------------------------------------------------
-// K2: exclusive scan of the per-coarse-tile counts (one workgroup; B*ncoarse is 256 per 1024^2 frame)
-
 
 // ------------------------------------------------------------------------------------------------
 // K3: fill the coarse bins.  Entry = {record index, bbox clamped to the coarse tile, 8 bits per side}.
@@ -478,34 +405,60 @@ __device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, i
 __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict__ recs,
                                                            const FaceData *__restrict__ fdata, int F, int cshift,
                                                            int nctx, int ncoarse, int64_t nrec,
-                                                           const uint64_t *__restrict__ coffset,
-                                                           uint32_t *__restrict__ ccursor, uint2 *__restrict__ bins,
-                                                           int64_t capacity, uint32_t *__restrict__ ccount,
-                                                           uint32_t *__restrict__ done, int64_t nc)
+                                                           const uint32_t *__restrict__ ccount,
+                                                           uint64_t *__restrict__ coffset, uint32_t *__restrict__ ccursor,
+                                                           uint2 *__restrict__ bins, int64_t frame_capacity)
 {
-    __shared__ uint32_t hist[kMaxCoarse];
-    __shared__ uint64_t base[kMaxCoarse];
+    extern __shared__ uint64_t fill_lds[];
+    uint64_t *base = fill_lds;                                                    // [ncoarse + 1]
+    uint32_t *hist = reinterpret_cast<uint32_t *>(fill_lds + ncoarse + 1);        // [ncoarse]
+    __shared__ uint64_t wave_sums[kBinThreads / 64];
     __shared__ BigQueue Q;
-    const int b = blockIdx.y, t = threadIdx.x;
+    const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t cb = (int64_t)b * ncoarse;
+    const uint64_t fbase = (uint64_t)b * (uint64_t)frame_capacity, fend = fbase + (uint64_t)frame_capacity;
+    // 1. the frame's bin offsets: exclusive scan of setup's per-tile totals, in every workgroup (a few
+    //    hundred L2-resident words; cheaper than a dependent scan launch or a device-wide ticket)
     {
-        // self-cleaning scratch: nothing reads the counts after setup's scan (the raster uses offset
-        // differences), so they and setup's ticket are returned to zero here for the next forward
-        const int64_t nblk = (int64_t)gridDim.x * gridDim.y, blk = (int64_t)b * gridDim.x + blockIdx.x;
-        for (int64_t k = blk * kBinThreads + t; k < nc; k += nblk * kBinThreads) ccount[k] = 0;
-        if (blk == 0 && t == 0) *done = 0;
+        const int per = (ncoarse + kBinThreads - 1) / kBinThreads, k0 = t * per, k1 = min(k0 + per, ncoarse);
+        uint64_t local = 0;
+        for (int k = k0; k < k1; ++k) {
+            const uint32_t v = ccount[cb + k];
+            hist[k] = v;
+            local += v;
+        }
+        uint64_t x = local;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wave_sums[wave] = x;
+        __syncthreads();
+        uint64_t run = fbase + (x - local);
+        for (int w = 0; w < wave; ++w) run += wave_sums[w];
+        for (int k = k0; k < k1; ++k) {
+            base[k] = run;
+            run += hist[k];
+        }
+        if (t == kBinThreads - 1) base[ncoarse] = run;  // the last thread owns the last (possibly empty) chunk
+        __syncthreads();
+        // the raster reads the offsets from memory (ncoarse + 1 per frame)
+        if (blockIdx.x == 0)
+            for (int k = t; k <= ncoarse; k += kBinThreads) coffset[(int64_t)b * (ncoarse + 1) + k] = base[k];
+        for (int k = t; k < ncoarse; k += kBinThreads) hist[k] = 0;
+        if (t == 0) Q.n = 0;
+        __syncthreads();
     }
-    for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
-    __syncthreads();
+    // 2. count this workgroup's pairs per coarse tile, reserve its range of each bin, place
     const Rec *frame_recs = recs + (int64_t)b * nrec;
-    if (t == 0) Q.n = 0;
     int nsub[kFacesPerThread];
     auto count = [&](int32_t, uint32_t, uint32_t, int cx, int cy) { atomicAdd(&hist[cy * nctx + cx], 1u); };
     auto place = [&](int32_t ri, uint32_t bx, uint32_t by, int cx, int cy) {
         const int c = cy * nctx + cx;
         const uint64_t dst = base[c] + atomicAdd(&hist[c], 1u);
-        if (dst < (uint64_t)capacity) bins[dst] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
+        if (dst < fend) bins[dst] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
     };
-    __syncthreads();
 #pragma unroll
     for (int q = 0; q < kFacesPerThread; ++q) {
         const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
@@ -518,10 +471,9 @@ __global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict
         }
     }
     coarse_pairs_flush<kBinThreads>(Q, count);
-    const int64_t cb = (int64_t)b * ncoarse;
     for (int c = t; c < ncoarse; c += kBinThreads) {
         const uint32_t n = hist[c];
-        if (n) base[c] = coffset[cb + c] + atomicAdd(&ccursor[cb + c], n);
+        if (n) base[c] += atomicAdd(&ccursor[cb + c], n);
         hist[c] = 0;
     }
     __syncthreads();
@@ -670,9 +622,9 @@ __device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
 __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
-                                                     uint32_t *__restrict__ ccursor,
+                                                     uint32_t *__restrict__ zcounts, int64_t nzcounts,
                                                      const uint64_t *__restrict__ coffset,
-                                                     const uint2 *__restrict__ bins, int64_t capacity,
+                                                     const uint2 *__restrict__ bins, int64_t frame_capacity,
                                                      int B, int H, int W, int Cdyn, int V, int F, int ntx, int cshift,
                                                      int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
                                                      int32_t *__restrict__ gbuffer, float *__restrict__ zero_a,
@@ -682,12 +634,12 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     if (!(AB & 16)) {
-        // housekeeping spread over all blocks (a few KB each): return fill's bin cursors to zero for
-        // the next forward, and zero-fill the caller's gradient accumulators if it passed them
+        // housekeeping spread over all blocks (a few KB each): return setup's bin counts and fill's
+        // cursors to zero for the next forward, and zero-fill the caller's gradient accumulators if it
+        // passed them
         const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
         const int64_t gt = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x, gs = nblk * 256;
-        const int64_t nc = (int64_t)B * ncoarse;
-        for (int64_t k = gt; k < nc; k += gs) ccursor[k] = 0;
+        for (int64_t k = gt; k < nzcounts; k += gs) zcounts[k] = 0;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (zero_a) {
             for (int64_t k = gt; k < (nzero_a >> 2); k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
@@ -730,7 +682,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const int si0 = tx * kTile, sj0 = ty * kTile + wave * 4;
     const int cx = si0 >> cshift, cy = sj0 >> cshift;
     const int c = cy * nctx + cx;
-    const int64_t cc = (int64_t)b * ncoarse + c;
+    const int64_t cc = (int64_t)b * (ncoarse + 1) + c;
     const uint64_t off = coffset[cc];
     const uint32_t cnt = (uint32_t)(coffset[cc + 1] - off);
     // strip rectangle relative to the coarse tile
@@ -739,7 +691,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
 
     if (AB & 8) {
         st.best_rec = (int32_t)(cnt + off);
-    } else if (off + cnt <= (uint64_t)capacity) {
+    } else if (off + cnt <= (uint64_t)(b + 1) * (uint64_t)frame_capacity) {
         int n_s = 0;
         for (uint32_t blk = 0;; blk += kFilterBlock) {
             const bool more = blk < cnt;
@@ -1642,38 +1594,35 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
     uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
     uint32_t *ccursor = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_cursor);
-    uint32_t *done = reinterpret_cast<uint32_t *>(sc + L.off_done);
     uint64_t *coffset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
     uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
     uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
-    const int64_t nc = (int64_t)B * L.ncoarse;
+    const int64_t nzcounts = (int64_t)((L.off_offset - L.off_count) / 4);
 
-    // counts, cursors and the setup ticket are adjacent: one memset, unless the caller vouches that
-    // they are zero (DIRT_FWD_SCRATCH_CLEAN, e.g. cleared by dirt_scratch_clear on a side stream)
+    // counts and cursors are adjacent: one memset, unless the caller vouches that they are zero
+    // (DIRT_FWD_SCRATCH_CLEAN: every forward's raster kernel returns them to zero)
     if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_offset - L.off_count, stream));
     const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     if (F > 0) {
-        ProfScope ps(K_SETUP, stream);
-        setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
-                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag,
-                                                                 done, coffset, nc);
+        {
+            ProfScope ps(K_SETUP, stream);
+            setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+                                                                     L.ncoarse, L.nrec, recs, fdata, ccount, flag);
+            HIP_TRY(hipGetLastError());
+        }
+        ProfScope ps(K_FILL, stream);
+        fill_kernel<<<bin_grid, dim3(kBinThreads), (size_t)L.ncoarse * 12 + 8, stream>>>(
+            recs, fdata, F, L.cshift, L.nctx, L.ncoarse, L.nrec, ccount, coffset, ccursor, bins, L.frame_capacity);
         HIP_TRY(hipGetLastError());
     } else {
-        ProfScope ps(K_SCAN, stream);
-        scan_kernel<<<dim3(1), dim3(kScanThreads), 0, stream>>>(ccount, coffset, nc);
-        HIP_TRY(hipGetLastError());
-    }
-    if (F > 0) {
-        ProfScope ps(K_FILL, stream);
-        fill_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(recs, fdata, F, L.cshift, L.nctx, L.ncoarse, L.nrec,
-                                                                coffset, ccursor, bins, L.bin_capacity, ccount, done, nc);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemsetAsync(coffset, 0, (size_t)(B * (int64_t)(L.ncoarse + 1)) * 8, stream));  // every bin empty
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
 #define LAUNCH_PROC(CC, SHT)                                                                                     \
     raster_kernel<CC, 0, SHT><<<grid, dim3(256), 0, stream>>>(                                                   \
-        background, vertex_colors, recs, fdata, ccursor, coffset, bins, L.bin_capacity, B, H, W, C, V, F, L.ntx,   \
+        background, vertex_colors, recs, fdata, ccount, nzcounts, coffset, bins, L.frame_capacity, B, H, W, C, V, F,\
+        L.ntx,                                                                                                     \
         L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices,                                  \
         zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                      \
         zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb)
@@ -1685,8 +1634,9 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     else if (shader_id >= DIRT_SHADER_OCEANIC)                                                                   \
         LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC);                                                                    \
     else                                                                                                         \
-    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,   \
-                                                      bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift,    \
+    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, nzcounts,   \
+                                                      coffset, bins, L.frame_capacity, B, H, W, C, V, F, L.ntx,   \
+                                                      L.cshift,                                                  \
                                                       L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices, \
                                                       zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
                                                       zero_grad_vertex_colors,                                     \
@@ -1786,7 +1736,8 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     const char *sv = static_cast<const char *>(saved), *sc = static_cast<const char *>(scratch);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
-    uint32_t *ccursor = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_cursor);
+    uint32_t *zc = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_count);
+    const int64_t nz = (int64_t)((L.off_offset - L.off_count) / 4);
     const uint64_t *coffset = reinterpret_cast<const uint64_t *>(sc + L.off_offset);
     const uint2 *bins = reinterpret_cast<const uint2 *>(sc + L.off_bins);
     hipEvent_t e0, e1;
@@ -1796,8 +1747,8 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
 #define V_RAST(AB)                                                                                                 \
     case AB:                                                                                                       \
-        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccursor, coffset,\
-                                                             bins, L.bin_capacity, B, H, W, C, V, F, L.ntx, L.cshift, \
+        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, zc, nz, coffset, \
+                                                             bins, L.frame_capacity, B, H, W, C, V, F, L.ntx, L.cshift,\
                                                              L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, 0,  \
                                                              nullptr, 0, nullptr, nullptr, 0, C);                    \
         break
