@@ -101,7 +101,7 @@ struct Layout {
     int cshift, csize;        // coarse tile edge = 1 << cshift pixels
     int nctx, ncty, ncoarse;  // coarse tiles per frame (<= kMaxCoarse)
     int64_t nrec;
-    size_t saved_recs, saved_fdata, saved_total;
+    size_t saved_recs, saved_fdata, saved_cov, saved_total;
     size_t off_count, off_cursor, off_offset, off_flag, off_bins, scratch_total;
     int64_t bin_capacity;
     int64_t frame_capacity;   // bins of frame b: [b * frame_capacity, (b + 1) * frame_capacity)
@@ -135,7 +135,8 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
                                       : default_capacity(B, F, L.ncoarse);
     L.saved_recs = 0;
     L.saved_fdata = (size_t)align_up((int64_t)B * L.nrec * (int64_t)sizeof(Rec), 256);
-    L.saved_total = L.saved_fdata + (size_t)align_up((int64_t)B * F * (int64_t)sizeof(FaceData), 256);
+    L.saved_cov = L.saved_fdata + (size_t)align_up((int64_t)B * F * (int64_t)sizeof(FaceData), 256);
+    L.saved_total = L.saved_cov + (size_t)align_up((int64_t)B * H * W, 256);  // 4 coverage bits per pixel
     const int64_t nc = (int64_t)B * L.ncoarse;
     size_t o = 0;
     L.frame_capacity = B > 0 ? L.bin_capacity / B : 0;
@@ -617,6 +618,32 @@ __device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
         }                                                                                                     \
     } while (0)
 
+__device__ __noinline__ bool covers_face_multi(int64_t hint_ri, const Rec *frame_recs, const FaceData *fdata_frame,
+                                               int F, int f, int i, int j);
+
+// Bit d of the result: the face visible at pixel (i, j) (record r, E = its edge values there) also
+// covers the neighbour in direction d (0 right, 1 left, 2 up, 3 down; window coordinates) -- exactly
+// the coverage tests of the backward's pairs, computed once here for every pixel, so the
+// backward reads them (its own face at p: bit d of p; the neighbour's face at p: bit opposite(d) of q)
+// instead of re-testing records per pair.
+__device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64_t E[3], bool multi, int32_t ri,
+                                                       const Rec *frame_recs, const FaceData *fdata_frame, int F, int f,
+                                                       int i, int j)
+{
+    uint32_t bits = 0;
+#pragma unroll
+    for (int dir = 0; dir < 4; ++dir) {
+        const int axis = dir >> 1, sg = (dir & 1) ? -1 : 1;
+        int64_t Eq[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Eq[k] = E[k] + (int64_t)(axis == 0 ? r.A[k] : r.B[k]) * (256 * sg);
+        bool c = inside(r, Eq);
+        if (!c && multi) c = covers_face_multi(ri, frame_recs, fdata_frame, F, f, i + (axis == 0 ? sg : 0), j + (axis == 1 ? sg : 0));
+        bits |= (c ? 1u : 0u) << dir;
+    }
+    return bits;
+}
+
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
@@ -627,7 +654,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                                                      const uint2 *__restrict__ bins, int64_t frame_capacity,
                                                      int B, int H, int W, int Cdyn, int V, int F, int ntx, int cshift,
                                                      int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
-                                                     int32_t *__restrict__ gbuffer, float *__restrict__ zero_a,
+                                                     int32_t *__restrict__ gbuffer, uint8_t *__restrict__ covbits,
+                                                     float *__restrict__ zero_a,
                                                      int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
                                                      const float *__restrict__ verts, const float *__restrict__ cam,
                                                      int sid, int tcb)
@@ -793,6 +821,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     }
     if (st.best_rec < 0) {
         gbuffer[o] = -1;
+        if constexpr (SH == DIRT_SHADER_GOURAUD) covbits[o] = 0;
 #pragma unroll
         for (int c2 = 0; c2 < CM; ++c2)
             if (c2 < C) out[c2] = kNoDepth ? 0.0f : bgv[c2];
@@ -859,6 +888,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         const float *cb = colors + (int64_t)b * V * C;
         const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
         for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
+        covbits[o] = (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, st.best_rec, frame_recs, fdata + (int64_t)b * F,
+                                                 F, face_of_record(st.best_rec, F), i, j);
     }
 }
 
@@ -1072,7 +1103,8 @@ __device__ __forceinline__ int run_start(int key, int lx)
 // 32 skip the DPP run scan (every lane adds into LDS)
 template <int CC, int AB = 0>
 __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
-                                                   const int32_t *__restrict__ gbuffer, const Rec *__restrict__ recs,
+                                                   const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
+                                                   const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
                                                    int V, int F, int ntx, int64_t nrec, float *__restrict__ grad_verts,
                                                    float *__restrict__ grad_colors, float *__restrict__ grad_bg,
@@ -1084,6 +1116,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     const int C = CC > 0 ? CC : Cdyn;
     const int NV = 9 + 3 * C;
     __shared__ int32_t s_gb[kHaloPix];
+    __shared__ uint8_t s_cov[kHaloPix];  // neighbour_coverage() bits of the pixel's face (forward)
     __shared__ int8_t s_slot[kHaloPix];  // slot of the pixel's record, -1 none, kNoSlot table full
     __shared__ float s_sx[kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), see DESIGN.md 4
     __shared__ float s_sy[kHaloPix];
@@ -1126,6 +1159,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
         // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * 256)
         static_assert(kHaloPix <= 512, "two staging passes");
         int32_t gbv[2];
+        uint32_t cvv[2];
         float Gv[2][CM], Iv[2][CM];
         bool ok[2];
 #pragma unroll
@@ -1134,9 +1168,11 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
             ok[u] = k < kHaloPix && hi >= 0 && hj >= 0 && hi < W && hj < H;
             gbv[u] = -2;
+            cvv[u] = 0;
             if (ok[u]) {
                 const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
                 gbv[u] = gbuffer[o];
+                cvv[u] = covbits[o];
 #pragma unroll
                 for (int c = 0; c < CM; ++c)
                     if (c < C) {
@@ -1150,6 +1186,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             const int k = t + 256 * u;
             if (k >= kHaloPix) continue;
             s_gb[k] = gbv[u];
+            s_cov[k] = (uint8_t)cvv[u];
             if (!ok[u]) continue;
             if constexpr (CM == 3) {
                 *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(Gv[u][0], Gv[u][1], Gv[u][2], 0.0f);
@@ -1169,22 +1206,15 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     const int32_t gp = in_frame ? s_gb[kme] : -2;
     {
         const int rt = (t & 63) * 4 + (t >> 6);  // 0..255 spread over the four waves
-        // own pixels first (run heads only; all distinct keys may not fit: the rest read global memory),
-        // then the 68 halo ring pixels
+        // the tile's own records (run heads only; all distinct keys may not fit: the rest read global
+        // memory).  The halo's records are not needed: pair coverage comes from the forward's bits.
+        (void)rt;
         const int32_t g = s_gb[kme];
         const int key = g >= 0 ? g : -1;
         const int start = run_start(key, lx);
         int slot = slot_insert_wave(T, key, key >= 0 && start == lx);
         slot = __shfl(slot, (t & 48) + start, 64);
         s_slot[kme] = key >= 0 ? slot : -1;
-        int kr = -1;
-        if (rt < 18) kr = rt;                                      // bottom row
-        else if (rt < 36) kr = (kHalo - 1) * kHalo + (rt - 18);    // top row
-        else if (rt < 52) kr = (rt - 35) * kHalo;                  // left column (rows 1..16)
-        else if (rt < 68) kr = (rt - 51) * kHalo + kHalo - 1;      // right column
-        const int32_t gr = kr >= 0 ? s_gb[kr] : -1;
-        const int sr = slot_insert_wave(T, gr, gr >= 0);
-        if (kr >= 0) s_slot[kr] = gr >= 0 ? sr : -1;
     }
     __syncthreads();
     PHASE_TS(2);
@@ -1322,30 +1352,10 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             } else if (AB & 16) {
                 code = 1u;
             } else {
-                bool mine_covers_other;
-                if (me_small) {
-                    int32_t e[3];
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) e[k] = eme[k] + (axis == 0 ? mA[k] : mB[k]) * (me_low ? 256 : -256);
-                    mine_covers_other = min(e[0], min(e[1], e[2])) > 0;
-                } else {
-                    const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
-                    int64_t Eq[3];
-                    edge_values(me, i + di, j + dj, Eq);
-                    mine_covers_other = inside(me, Eq);
-                }
-                if (!mine_covers_other && multi)
-                    mine_covers_other = covers_face_multi(rp, frame_recs, fdata_frame, F, f, i + di, j + dj);
-                const int sq = s_slot[kq];
-                bool other_covers_me;
-                if (sq >= 0 && !slot_is_large(T, sq)) {
-                    other_covers_me = slot_covers_small(T, sq, hx, hy, i, j);
-                } else {
-                    const EdgePart other = *reinterpret_cast<const EdgePart *>(&frame_recs[rq]);
-                    other_covers_me = edge_covers(other, i, j);
-                }
-                if (!other_covers_me && (gq & kGbufMulti))
-                    other_covers_me = covers_face_multi(rq, frame_recs, fdata_frame, F, fq, i, j);
+                // the forward's neighbour_coverage(): my face at q (bit dir of p), q's face at p (bit
+                // opposite(dir) of q; opposite flips bit 0 of dir)
+                const bool mine_covers_other = (s_cov[kme] >> dir) & 1u;
+                const bool other_covers_me = (s_cov[kq] >> (dir ^ 1)) & 1u;
                 code = (!mine_covers_other && other_covers_me) ? 2u : (mine_covers_other && !other_covers_me) ? 0u : 1u;
             }
             codes |= code << (2 * dir);
@@ -1592,6 +1602,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     char *sv = static_cast<char *>(saved), *sc = static_cast<char *>(scratch);
     Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
     FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
+    uint8_t *covbits = reinterpret_cast<uint8_t *>(sv + L.saved_cov);
     uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
     uint32_t *ccursor = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_cursor);
     uint64_t *coffset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
@@ -1623,7 +1634,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     raster_kernel<CC, 0, SHT><<<grid, dim3(256), 0, stream>>>(                                                   \
         background, vertex_colors, recs, fdata, ccount, nzcounts, coffset, bins, L.frame_capacity, B, H, W, C, V, F,\
         L.ntx,                                                                                                     \
-        L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices,                                  \
+        L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                         \
         zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                      \
         zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb)
 #define LAUNCH_RASTER(CC)                                                                                        \
@@ -1637,7 +1648,8 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, nzcounts,   \
                                                       coffset, bins, L.frame_capacity, B, H, W, C, V, F, L.ntx,   \
                                                       L.cshift,                                                  \
-                                                      L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, zero_grad_vertices, \
+                                                      L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits,          \
+                                                      zero_grad_vertices,                                          \
                                                       zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
                                                       zero_grad_vertex_colors,                                     \
                                                       zero_grad_vertex_colors ? (int64_t)B * V * C : 0,            \
@@ -1702,6 +1714,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     const char *sv = static_cast<const char *>(saved);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    const uint8_t *covbits = reinterpret_cast<const uint8_t *>(sv + L.saved_cov);
     if (V > 0 && !(flags & DIRT_BWD_ACCUMULATE)) {
         const int64_t na = (int64_t)B * V * 4, nb = (int64_t)B * V * C;
         const int64_t blocks = std::min<int64_t>(2048, (na / 4 + 255) / 256 + 1);
@@ -1711,7 +1724,8 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_GRAD, stream);
 #define LAUNCH_GRAD(CC)                                                                                       \
-    grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, recs, fdata, B, H, W, C, V, F, \
+    grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, \
+                                                    V, F,                                                        \
                                                     L.ntx, L.nrec, grad_vertices, grad_vertex_colors,            \
                                                     grad_background, ndc_scale(W, H))
     if (C == 1) LAUNCH_GRAD(1);
@@ -1736,6 +1750,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     const char *sv = static_cast<const char *>(saved), *sc = static_cast<const char *>(scratch);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    uint8_t *covbits = reinterpret_cast<uint8_t *>(const_cast<char *>(sv) + L.saved_cov);
     uint32_t *zc = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_count);
     const int64_t nz = (int64_t)((L.off_offset - L.off_count) / 4);
     const uint64_t *coffset = reinterpret_cast<const uint64_t *>(sc + L.off_offset);
@@ -1749,7 +1764,8 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     case AB:                                                                                                       \
         raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, zc, nz, coffset, \
                                                              bins, L.frame_capacity, B, H, W, C, V, F, L.ntx, L.cshift,\
-                                                             L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, 0,  \
+                                                             L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits,     \
+                                                             nullptr, 0,                                              \
                                                              nullptr, 0, nullptr, nullptr, 0, C);                    \
         break
     switch (variant) {
@@ -1781,6 +1797,7 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     const char *sv = static_cast<const char *>(saved);
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    const uint8_t *covbits = reinterpret_cast<const uint8_t *>(sv + L.saved_cov);
     HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)B * V * 4 * sizeof(float), stream));
     HIP_TRY(hipMemsetAsync(grad_vertex_colors, 0, (size_t)B * V * C * sizeof(float), stream));
     hipEvent_t e0, e1;
@@ -1790,7 +1807,8 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
 #define V_GRAD(AB)                                                                                                   \
     case AB:                                                                                                         \
-        grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, recs, fdata, B, H, W, C, V, \
+        grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W,\
+                                                           C, V,                                                     \
                                                            F, L.ntx, L.nrec, grad_vertices, grad_vertex_colors,     \
                                                            grad_background, ndc_scale(W, H));                        \
         break
