@@ -516,41 +516,57 @@ __device__ __forceinline__ int xcd_tile(int x, int n)
     return g * q + min(g, r) + k;
 }
 
-constexpr int kSmallEdge = 1 << 16;
 constexpr int kListCap = 256;      // per-wave survivor list (filtered record indices)
 constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per round (2 loads per lane in flight)
-constexpr int32_t kLargeFlag = (int32_t)0x80000000;
+// A staged record is "small" when every |A|, |B| < 2^15: its edge steps inside a strip are one
+// v_dot2_i32_i16 of the packed (A, B) with the lane's packed (dx, dy) offsets (<= 15*256, 3*256).
+constexpr int kDotEdge = 1 << 15;
+constexpr uint32_t kLargeAB = 0x80008000u;  // ab[0] of a large entry (A = B = -2^15 never occurs in a small one)
 
-struct alignas(16) StripEntry {  // 64 B of wave-private LDS per staged triangle
-    int32_t e[3];
-    int32_t A[3];
-    int32_t B[3];
-    float za, zb, fx0, fy0, z0;
-    int32_t face;
-    int32_t ri;  // record index; kLargeFlag set -> per-lane int64 path
+struct alignas(16) StripEntry {  // 48 B of wave-private LDS per staged (sub-)triangle: three ds_read_b128
+    int32_t e[3];    // small: E + owned at the strip origin (2^30 when the edge holds over the whole strip);
+                     // large: e[0] = record index
+    uint32_t ab[3];  // small: (uint16)A | B << 16; large: ab[0] = kLargeAB
+    float za, zb, fx0, fy0, z0;  // fx0, fy0 8-byte aligned: one register pair for v_pk_add_f32
+    uint32_t key;    // face << 3 | sub-triangle: the low word of the depth key (the lower face wins ties)
 };
-static_assert(sizeof(StripEntry) == 64, "StripEntry must be 64 B");
+static_assert(sizeof(StripEntry) == 48, "StripEntry must be 48 B");
 
-struct PixelState {
-    uint64_t best;
-    int32_t best_rec;
-};
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef int int4v __attribute__((ext_vector_type(4)));
 
-// NoDepth: GL_DEPTH_TEST off (hill.cpp:194): the last face in draw order wins, near/far clipping stays
-template <bool NoDepth = false>
-__device__ __forceinline__ void depth_update(float za, float zb, float fx0, float fy0, float z0, int32_t face,
-                                             int32_t ri, float fxl, float fyl, PixelState &st)
+// low word of the depth key of record ri: face << 3 | sub-triangle index (rec_index inverse)
+__device__ __forceinline__ uint32_t rec_key(int32_t ri, int F)
 {
-    // R4, same operation order as sample_depth()
-    const float zw = (za * (fxl - fx0) + zb * (fyl - fy0)) + z0;
-    if (!(zw >= 0.0f && zw <= 1.0f)) return;
-    const uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
-    if (!NoDepth && q >= kDepthMax) return;
-    const uint64_t key = NoDepth ? (uint64_t)(0xffffffffu - (uint32_t)face) : (((uint64_t)q << 32) | (uint32_t)face);
-    if (key < st.best) {
-        st.best = key;
-        st.best_rec = ri;
-    }
+    if (ri < F) return (uint32_t)ri << 3;
+    const int32_t d = ri - F, f = d / kExtraPerFace;
+    return ((uint32_t)f << 3) | (uint32_t)(d - f * kExtraPerFace + 1);
+}
+__device__ __forceinline__ int32_t key_rec(uint32_t key, int F) { return (int32_t)rec_index(F, (int)(key >> 3), (int)(key & 7)); }
+
+// R4 key: (q24 << 32 | face << 3 | s), minimum wins -- GL LESS with draw order = face index
+// (rasterise_egl.cpp:451-457).  NoDepth (hill.cpp:194, GL_DEPTH_TEST off): the last face in draw order
+// wins, near/far clipping stays.  The initial value rejects q >= 2^24-1 (cleared depth 1.0) by itself.
+template <bool NoDepth>
+__device__ __forceinline__ uint64_t depth_key(uint32_t q, uint32_t key)
+{
+    return NoDepth ? (uint64_t)(0xffffffffu - key) : (((uint64_t)q << 32) | key);
+}
+template <bool NoDepth>
+constexpr uint64_t kKeyInit = NoDepth ? ~0ull : ((uint64_t)kDepthMax << 32);
+template <bool NoDepth>
+__device__ __forceinline__ uint32_t key_low(uint64_t best) { return NoDepth ? 0xffffffffu - (uint32_t)best : (uint32_t)best; }
+
+// overflow / large-record path: one record against this lane's pixel (R3 + R4)
+template <bool NoDepth>
+__device__ __forceinline__ void depth_update(const Rec &r, uint32_t key, float fxl, float fyl, bool in, uint64_t &best)
+{
+    const float zw = depth_at(r.za, r.zb, r.z0, fxl - r.fx0, fyl - r.fy0);
+    const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
+    const uint64_t k = depth_key<NoDepth>(depth_q24(zc), key);
+    const bool win = in && zc == zw && k < best;
+    best = win ? k : best;
 }
 
 __device__ __forceinline__ void wave_lds_sync()
@@ -561,9 +577,10 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Stage up to 64 survivors (s_list[from .. from+m)) into entries; returns number staged.
+// Stage up to 64 survivors (s_list[from .. from+m)) into entries; returns number staged, `large` = some
+// staged entry takes the int64 path.
 __device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_list, int from, int m, int si0, int sj0,
-                           StripEntry *ent, int lane)
+                           int F, StripEntry *ent, int lane, bool &large)
 {
     bool keep = false;
     StripEntry E;
@@ -573,7 +590,7 @@ __device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_
         bool small = true;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-            small = small && R.A[k] > -kSmallEdge && R.A[k] < kSmallEdge && R.B[k] > -kSmallEdge && R.B[k] < kSmallEdge;
+            small = small && R.A[k] > -kDotEdge && R.A[k] < kDotEdge && R.B[k] > -kDotEdge && R.B[k] < kDotEdge;
         keep = true;
         const int32_t px0 = si0 * 256 + 128, py0 = sj0 * 256 + 128;
 #pragma unroll
@@ -585,19 +602,61 @@ __device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_
             const int64_t emax = e0 + (sx > 0 ? sx : 0) + (sy > 0 ? sy : 0);
             if (emax <= 0) keep = false;
             E.e[k] = emin > 0 ? (1 << 30) : (int32_t)e0;
-            E.A[k] = R.A[k];
-            E.B[k] = R.B[k];
+            E.ab[k] = ((uint32_t)R.A[k] & 0xffffu) | ((uint32_t)R.B[k] << 16);
         }
-        E.za = R.za; E.zb = R.zb; E.fx0 = R.fx0; E.fy0 = R.fy0; E.z0 = R.z0;
-        E.face = R.face;
-        E.ri = small ? ri : (ri | kLargeFlag);
+        if (!small) {
+            E.e[0] = ri;
+            E.ab[0] = kLargeAB;
+        }
+        E.za = R.za; E.zb = R.zb; E.z0 = R.z0; E.fx0 = R.fx0; E.fy0 = R.fy0;
+        E.key = rec_key(ri, F);
     }
     const uint64_t mask = __ballot(keep);
+    large = __ballot(keep && E.ab[0] == kLargeAB) != 0;
     if (keep) {
         const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        ent[pos] = E;
+        int4 *d = reinterpret_cast<int4 *>(&ent[pos]);
+        d[0] = make_int4(E.e[0], E.e[1], E.e[2], (int)E.ab[0]);
+        d[1] = make_int4((int)E.ab[1], (int)E.ab[2], __float_as_int(E.za), __float_as_int(E.zb));
+        d[2] = make_int4(__float_as_int(E.fx0), __float_as_int(E.fy0), __float_as_int(E.z0), (int)E.key);
     }
     return __popcll(mask);
+}
+
+// The per-pixel loop over ne staged entries: R3 coverage + R4 depth, min key per lane.  Large: some
+// entries need the int64 edge path (chosen per entry, wave-uniform); otherwise the loop has no branch.
+template <bool NoDepth, bool Large>
+__device__ __forceinline__ void raster_entries(const int4 *__restrict__ ent4, int ne, const Rec *__restrict__ frame_recs,
+                                               short2v pix, float2v pxy, int i, int j, uint64_t &best)
+{
+    for (int e = 0; e < ne; ++e) {
+        // three 16-B broadcast reads (volatile: keeps them whole ds_read_b128s, 4 LDS cycles each)
+        typedef __attribute__((address_space(3))) const volatile int4v lds_int4v;
+        lds_int4v *ve = (lds_int4v *)(ent4) + 3 * e;
+        const int4v q0 = ve[0], q1 = ve[1], q2 = ve[2];
+        bool in;
+        if (!Large || __builtin_amdgcn_readfirstlane(q0.w) != (int)kLargeAB) {
+            // R3 on strip-relative exact int32 values: E + owned > 0 for all three edges
+            // (scalars first: clang's __builtin_bit_cast of an ext_vector component reads component 0)
+            const int ab0 = q0.w, ab1 = q1.x, ab2 = q1.y;
+            const int e0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab0), pix, q0.x, false);
+            const int e1 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab1), pix, q0.y, false);
+            const int e2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab2), pix, q0.z, false);
+            in = min(e0, min(e1, e2)) > 0;
+        } else {
+            const Rec &r = frame_recs[__builtin_amdgcn_readfirstlane(q0.x)];
+            int64_t E[3];
+            edge_values(r, i, j, E);
+            in = inside(r, E);
+        }
+        // R4 without branches: in range iff the clamp leaves zw unchanged (false for NaN)
+        const float2v d = pxy - float2v{__int_as_float(q2.x), __int_as_float(q2.y)};
+        const float zw = depth_at(__int_as_float(q1.z), __int_as_float(q1.w), __int_as_float(q2.z), d.x, d.y);
+        const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
+        const uint64_t k = depth_key<NoDepth>(depth_q24(zc), (uint32_t)q2.w);
+        const bool win = in && zc == zw && k < best;
+        best = win ? k : best;
+    }
 }
 
 // per-workgroup phase timestamps of the instrumented backward (AB & 128, dirt_debug_bwd_variant 128)
@@ -706,7 +765,9 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
             if (c < C) bgv[c] = background[o * C + c];
     }
 
-    PixelState st{~0ull, -1};
+    uint64_t best = kKeyInit<kNoDepth>;
+    const short2v pix = {(short)dx, (short)dy};  // lane offset from the strip origin in sub-pixels
+    const float2v pxy = {fxl, fyl};
     const int si0 = tx * kTile, sj0 = ty * kTile + wave * 4;
     const int cx = si0 >> cshift, cy = sj0 >> cshift;
     const int c = cy * nctx + cx;
@@ -718,7 +779,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const uint32_t ry0 = (uint32_t)(sj0 - (cy << cshift)), ry1 = ry0 + 3;
 
     if (AB & 8) {
-        st.best_rec = (int32_t)(cnt + off);
+        best = cnt + off;
     } else if (off + cnt <= (uint64_t)(b + 1) * (uint64_t)frame_capacity) {
         int n_s = 0;
         for (uint32_t blk = 0;; blk += kFilterBlock) {
@@ -752,7 +813,7 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
             if (n_s < kListCap - kFilterBlock && more) continue;
             wave_lds_sync();
             if (AB & 2) {
-                st.best_rec += s_list[lane & (kListCap - 1)] + n_s;
+                best += (uint64_t)(s_list[lane & (kListCap - 1)] + n_s);
                 n_s = 0;
                 if (!more) break;
                 continue;
@@ -760,38 +821,17 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
             // b + c: stage and rasterise the collected survivors, 64 at a time
             for (int from = 0; from < n_s; from += 64) {
                 const int m = min(64, n_s - from);
-                const int ne = stage_strip(frame_recs, s_list, from, m, si0, sj0, s_ent, lane);
+                bool large;
+                const int ne = stage_strip(frame_recs, s_list, from, m, si0, sj0, F, s_ent, lane, large);
                 wave_lds_sync();
                 if (AB & 1) {
-                    if (ne > 0) st.best_rec += s_ent[lane % ne].face;
+                    if (ne > 0) best += s_ent[lane % ne].key;
                     wave_lds_sync();
                     continue;
                 }
-                for (int e = 0; e < ne; ++e) {
-                    const StripEntry R = s_ent[e];  // one 64-B broadcast read
-                    const int32_t rif = __builtin_amdgcn_readfirstlane(R.ri);
-                    bool in;
-                    if (rif >= 0) {
-                        const int32_t e0 = R.e[0] + __mul24(R.A[0], dx) + __mul24(R.B[0], dy);
-                        const int32_t e1 = R.e[1] + __mul24(R.A[1], dx) + __mul24(R.B[1], dy);
-                        const int32_t e2 = R.e[2] + __mul24(R.A[2], dx) + __mul24(R.B[2], dy);
-                        in = min(e0, min(e1, e2)) > 0;
-                    } else {
-                        const Rec &r = frame_recs[rif & 0x7fffffff];
-                        int64_t E[3];
-                        edge_values(r, i, j, E);
-                        in = inside(r, E);
-                    }
-                    // R4 without branches (same operation order as sample_depth)
-                    const float zw = (R.za * (fxl - R.fx0) + R.zb * (fyl - R.fy0)) + R.z0;
-                    const uint32_t q = (uint32_t)(__builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f) * 16777215.0f + 0.5f);
-                    const bool ok = in && zw >= 0.0f && zw <= 1.0f && (kNoDepth || q < kDepthMax);
-                    const uint64_t key = kNoDepth ? (uint64_t)(0xffffffffu - (uint32_t)R.face)
-                                                  : (((uint64_t)q << 32) | (uint32_t)R.face);
-                    const bool win = ok && key < st.best;
-                    st.best = win ? key : st.best;
-                    st.best_rec = win ? (rif & 0x7fffffff) : st.best_rec;
-                }
+                const int4 *ent4 = reinterpret_cast<const int4 *>(s_ent);
+                if (large) raster_entries<kNoDepth, true>(ent4, ne, frame_recs, pix, pxy, i, j, best);
+                else raster_entries<kNoDepth, false>(ent4, ne, frame_recs, pix, pxy, i, j, best);
                 wave_lds_sync();
             }
             n_s = 0;
@@ -807,19 +847,19 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
                 if (r.i0 > r.i1) continue;
                 int64_t E[3];
                 edge_values(r, i, j, E);
-                if (!inside(r, E)) continue;
-                depth_update<kNoDepth>(r.za, r.zb, r.fx0, r.fy0, r.z0, r.face, (int32_t)ri, fxl, fyl, st);
+                depth_update<kNoDepth>(r, ((uint32_t)f << 3) | (uint32_t)s, fxl, fyl, inside(r, E), best);
             }
         }
     }
 
     if (!in_frame) return;
     float *out = pixels + o * C;
-    if (AB & 7) {
-        gbuffer[o] = st.best_rec;
+    if (AB & 15) {
+        gbuffer[o] = (int32_t)best;
         return;
     }
-    if (st.best_rec < 0) {
+    const int32_t best_rec = best != kKeyInit<kNoDepth> ? key_rec(key_low<kNoDepth>(best), F) : -1;
+    if (best_rec < 0) {
         gbuffer[o] = -1;
         if constexpr (SH == DIRT_SHADER_GOURAUD) covbits[o] = 0;
 #pragma unroll
@@ -827,9 +867,9 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
             if (c2 < C) out[c2] = kNoDepth ? 0.0f : bgv[c2];
         return;
     }
-    const Rec &r = frame_recs[st.best_rec];
-    const FaceData fd = fdata[(int64_t)b * F + face_of_record(st.best_rec, F)];
-    gbuffer[o] = st.best_rec | (fd.clipped ? kGbufMulti : 0);
+    const Rec &r = frame_recs[best_rec];
+    const FaceData fd = fdata[(int64_t)b * F + face_of_record(best_rec, F)];
+    gbuffer[o] = best_rec | (fd.clipped ? kGbufMulti : 0);
     int64_t E[3];
     edge_values(r, i, j, E);
     float lam[3] = {0.0f, 0.0f, 0.0f};
@@ -888,8 +928,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
         const float *cb = colors + (int64_t)b * V * C;
         const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
         for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
-        covbits[o] = (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, st.best_rec, frame_recs, fdata + (int64_t)b * F,
-                                                 F, face_of_record(st.best_rec, F), i, j);
+        covbits[o] = (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, best_rec, frame_recs, fdata + (int64_t)b * F,
+                                                 F, face_of_record(best_rec, F), i, j);
     }
 }
 

@@ -167,26 +167,37 @@ __device__ __forceinline__ bool inside(const R &r, const int64_t E[3])
     return in;
 }
 
+// R4: depth at the pixel centre, zw = fma(za, fx - fx0, fma(zb, fy - fy0, z0)) (fx - fx0 is exact: both
+// are multiples of 2^-8 below 2^15), in range iff 0 <= zw <= 1; quantised q = (uint)fma(zw, 2^24-1, 0.5)
+__device__ __forceinline__ float depth_at(float za, float zb, float z0, float dx, float dy)
+{
+    return __builtin_fmaf(za, dx, __builtin_fmaf(zb, dy, z0));
+}
+
+__device__ __forceinline__ uint32_t depth_q24(float zw) { return (uint32_t)__builtin_fmaf(zw, 16777215.0f, 0.5f); }
+
 // R4: 24-bit depth of the sample, false if outside [0,1] or not nearer than the cleared depth
 template <typename R>
 __device__ __forceinline__ bool sample_depth(const R &r, int i, int j, uint32_t &d)
 {
     const float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
-    const float zw = (r.za * (fx - r.fx0) + r.zb * (fy - r.fy0)) + r.z0;
+    const float zw = depth_at(r.za, r.zb, r.z0, fx - r.fx0, fy - r.fy0);
     if (!(zw >= 0.0f && zw <= 1.0f)) return false;
-    const uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
+    const uint32_t q = depth_q24(zw);
     if (q >= kDepthMax) return false;
     d = q;
     return true;
 }
 
-// R6: perspective-correct parent barycentrics from edge values (or sums of two edge values)
+// R6: perspective-correct parent barycentrics from edge values (or sums of two edge values):
+// a_k = E_k / w_k, m_k = a_k * (1 / ((a0 + a1) + a2)) (one correctly rounded division), mapped through the basis
 __device__ __forceinline__ bool parent_lambda(const Rec &r, const int64_t E[3], float lam[3])
 {
     const float a0 = (float)E[0] * r.iw[0], a1 = (float)E[1] * r.iw[1], a2 = (float)E[2] * r.iw[2];
     const float s = (a0 + a1) + a2;
     if (s == 0.0f) return false;
-    const float m0 = a0 / s, m1 = a1 / s, m2 = a2 / s;
+    const float rs = 1.0f / s;
+    const float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
 #pragma unroll
     for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
     return true;

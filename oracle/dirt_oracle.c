@@ -231,9 +231,9 @@ static inline int inside(const orc_rec *r, const int64_t E[3])
 static inline int sample_depth(const orc_rec *r, int i, int j, uint32_t *d)
 {
     float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
-    float zw = (r->za * (fx - r->fx0) + r->zb * (fy - r->fy0)) + r->z0;
+    float zw = fmaf(r->za, fx - r->fx0, fmaf(r->zb, fy - r->fy0, r->z0));
     if (!(zw >= 0.0f && zw <= 1.0f)) return 0;
-    uint32_t q = (uint32_t)(zw * 16777215.0f + 0.5f);
+    uint32_t q = (uint32_t)fmaf(zw, 16777215.0f, 0.5f);
     if (q >= DEPTH_MAX) return 0;
     *d = q;
     return 1;
@@ -243,7 +243,7 @@ static inline int sample_depth(const orc_rec *r, int i, int j, uint32_t *d)
 static inline int sample_in_range(const orc_rec *r, int i, int j)
 {
     float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
-    float zw = (r->za * (fx - r->fx0) + r->zb * (fy - r->fy0)) + r->z0;
+    float zw = fmaf(r->za, fx - r->fx0, fmaf(r->zb, fy - r->fy0, r->z0));
     return zw >= 0.0f && zw <= 1.0f;
 }
 
@@ -253,7 +253,8 @@ static inline int parent_lambda(const orc_rec *r, const int64_t E[3], float lam[
     float a0 = (float)E[0] * r->iw[0], a1 = (float)E[1] * r->iw[1], a2 = (float)E[2] * r->iw[2];
     float s = (a0 + a1) + a2;
     if (s == 0.0f) return 0;
-    float m0 = a0 / s, m1 = a1 / s, m2 = a2 / s;
+    float rs = 1.0f / s;
+    float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
     for (int i = 0; i < 3; ++i) lam[i] = (m0 * r->basis[0 * 3 + i] + m1 * r->basis[1 * 3 + i]) + m2 * r->basis[2 * 3 + i];
     return 1;
 }

@@ -46,7 +46,8 @@ def main():
     rfn = lib.dirt_debug_raster_variant
     rfn.argtypes = [ctypes.c_int, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, P, ctypes.POINTER(ctypes.c_float)]
     rfn.restype = ctypes.c_int
-    RN = {0: "full", 1: "no pixel loop", 2: "bin filter only", 4: "no resolve", 8: "nothing (io only)"}
+    RN = {0: "full", 1: "no pixel loop, no resolve", 2: "bin filter only, no resolve", 4: "no resolve",
+          8: "nothing (housekeeping + bg prefetch + gbuffer write)"}
     rres = {k: [] for k in RN}
     for rnd in range(30):
         for k in RN:
