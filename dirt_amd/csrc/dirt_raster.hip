@@ -516,8 +516,7 @@ __device__ __forceinline__ int xcd_tile(int x, int n)
     return g * q + min(g, r) + k;
 }
 
-constexpr int kListCap = 256;      // per-wave survivor list (filtered record indices)
-constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per round (2 loads per lane in flight)
+constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per wave and chunk (2 loads per lane in flight)
 // A staged record is "small" when every |A|, |B| < 2^15: its edge steps inside a strip are one
 // v_dot2_i32_i16 of the packed (A, B) with the lane's packed (dx, dy) offsets (<= 15*256, 3*256).
 constexpr int kDotEdge = 1 << 15;
@@ -577,86 +576,87 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Stage up to 64 survivors (s_list[from .. from+m)) into entries; returns number staged, `large` = some
-// staged entry takes the int64 path.
-__device__ int stage_strip(const Rec *__restrict__ frame_recs, const int32_t *s_list, int from, int m, int si0, int sj0,
-                           int F, StripEntry *ent, int lane, bool &large)
+// Stage one tile survivor (record ri) for the 16x16 tile at pixel (ti0, tj0): edge values at the tile
+// origin (E + owned, exact int32, pinned to 2^30 where the edge holds over the whole tile), the packed
+// (A, B) steps, depth plane and key.  Returns the mask of the tile's four 16x4 strips the record can
+// cover (its rows overlap the strip and no edge excludes the whole strip; exact int64 tests) and sets
+// `large` when the record needs the per-lane int64 path (some |A|, |B| >= 2^15).
+__device__ __forceinline__ uint32_t stage_tile(const Rec *__restrict__ frame_recs, int32_t ri, int ti0, int tj0, int F,
+                                               StripEntry &E, bool &large)
 {
-    bool keep = false;
-    StripEntry E;
-    if (lane < m) {
-        const int32_t ri = s_list[from + lane];
-        const RasterPart R = *reinterpret_cast<const RasterPart *>(&frame_recs[ri]);
-        bool small = true;
+    const RasterPart R = *reinterpret_cast<const RasterPart *>(&frame_recs[ri]);
+    bool small = true;
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-            small = small && R.A[k] > -kDotEdge && R.A[k] < kDotEdge && R.B[k] > -kDotEdge && R.B[k] < kDotEdge;
-        keep = true;
-        const int32_t px0 = si0 * 256 + 128, py0 = sj0 * 256 + 128;
+    for (int k = 0; k < 3; ++k)
+        small = small && R.A[k] > -kDotEdge && R.A[k] < kDotEdge && R.B[k] > -kDotEdge && R.B[k] < kDotEdge;
+    uint32_t mask = 0;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
-            const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
-            const int64_t sx = (int64_t)R.A[k] * (15 * 256), sy = (int64_t)R.B[k] * (3 * 256);
-            const int64_t emin = e0 + (sx < 0 ? sx : 0) + (sy < 0 ? sy : 0);
-            const int64_t emax = e0 + (sx > 0 ? sx : 0) + (sy > 0 ? sy : 0);
-            if (emax <= 0) keep = false;
-            E.e[k] = emin > 0 ? (1 << 30) : (int32_t)e0;
-            E.ab[k] = ((uint32_t)R.A[k] & 0xffffu) | ((uint32_t)R.B[k] << 16);
-        }
-        if (!small) {
-            E.e[0] = ri;
-            E.ab[0] = kLargeAB;
-        }
-        E.za = R.za; E.zb = R.zb; E.z0 = R.z0; E.fx0 = R.fx0; E.fy0 = R.fy0;
-        E.key = rec_key(ri, F);
+    for (int st = 0; st < kStrips; ++st) {
+        const int sj0 = tj0 + 4 * st;
+        if ((int)R.j0 <= sj0 + 3 && (int)R.j1 >= sj0) mask |= 1u << st;
     }
-    const uint64_t mask = __ballot(keep);
-    large = __ballot(keep && E.ab[0] == kLargeAB) != 0;
-    if (keep) {
-        const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        int4 *d = reinterpret_cast<int4 *>(&ent[pos]);
-        d[0] = make_int4(E.e[0], E.e[1], E.e[2], (int)E.ab[0]);
-        d[1] = make_int4((int)E.ab[1], (int)E.ab[2], __float_as_int(E.za), __float_as_int(E.zb));
-        d[2] = make_int4(__float_as_int(E.fx0), __float_as_int(E.fy0), __float_as_int(E.z0), (int)E.key);
+    const int32_t px0 = ti0 * 256 + 128, py0 = tj0 * 256 + 128;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
+        const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
+        const int64_t sx = (int64_t)R.A[k] * (15 * 256), by = (int64_t)R.B[k] * (4 * 256);
+        const int64_t xmax = sx > 0 ? sx : 0, xmin = sx < 0 ? sx : 0;
+        const int64_t ymax3 = by > 0 ? 3 * (by >> 2) : 0, ymin15 = by < 0 ? 15 * (by >> 2) : 0;
+#pragma unroll
+        for (int st = 0; st < kStrips; ++st)
+            if (e0 + xmax + st * by + ymax3 <= 0) mask &= ~(1u << st);
+        E.e[k] = e0 + xmin + ymin15 > 0 ? (1 << 30) : (int32_t)e0;
+        E.ab[k] = ((uint32_t)R.A[k] & 0xffffu) | ((uint32_t)R.B[k] << 16);
     }
-    return __popcll(mask);
+    if (!small) {
+        E.e[0] = ri;
+        E.ab[0] = kLargeAB;
+    }
+    E.za = R.za; E.zb = R.zb; E.z0 = R.z0; E.fx0 = R.fx0; E.fy0 = R.fy0;
+    E.key = rec_key(ri, F);
+    large = !small;
+    return mask;
 }
 
-// The per-pixel loop over ne staged entries: R3 coverage + R4 depth, min key per lane.  Large: some
-// entries need the int64 edge path (chosen per entry, wave-uniform); otherwise the loop has no branch.
-template <bool NoDepth, bool Large>
-__device__ __forceinline__ void raster_entries(const int4 *__restrict__ ent4, int ne, const Rec *__restrict__ frame_recs,
-                                               short2v pix, float2v pxy, int i, int j, uint64_t &best)
+// R3 + R4 of staged entries (LDS, three 16-B broadcast reads each) against this lane's pixel
+typedef __attribute__((address_space(3))) const volatile int4v lds_int4v;
+struct EntryRegs {
+    int4v q0, q1, q2;
+};
+// volatile + LDS address space: keeps the reads whole ds_read_b128s (4 LDS cycles each)
+__device__ __forceinline__ EntryRegs load_entry(const StripEntry *ent, int e)
 {
-    for (int e = 0; e < ne; ++e) {
-        // three 16-B broadcast reads (volatile: keeps them whole ds_read_b128s, 4 LDS cycles each)
-        typedef __attribute__((address_space(3))) const volatile int4v lds_int4v;
-        lds_int4v *ve = (lds_int4v *)(ent4) + 3 * e;
-        const int4v q0 = ve[0], q1 = ve[1], q2 = ve[2];
-        bool in;
-        if (!Large || __builtin_amdgcn_readfirstlane(q0.w) != (int)kLargeAB) {
-            // R3 on strip-relative exact int32 values: E + owned > 0 for all three edges
-            // (scalars first: clang's __builtin_bit_cast of an ext_vector component reads component 0)
-            const int ab0 = q0.w, ab1 = q1.x, ab2 = q1.y;
-            const int e0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab0), pix, q0.x, false);
-            const int e1 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab1), pix, q0.y, false);
-            const int e2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab2), pix, q0.z, false);
-            in = min(e0, min(e1, e2)) > 0;
-        } else {
-            const Rec &r = frame_recs[__builtin_amdgcn_readfirstlane(q0.x)];
-            int64_t E[3];
-            edge_values(r, i, j, E);
-            in = inside(r, E);
-        }
-        // R4 without branches: in range iff the clamp leaves zw unchanged (false for NaN)
-        const float2v d = pxy - float2v{__int_as_float(q2.x), __int_as_float(q2.y)};
-        const float zw = depth_at(__int_as_float(q1.z), __int_as_float(q1.w), __int_as_float(q2.z), d.x, d.y);
-        const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
-        const uint64_t k = depth_key<NoDepth>(depth_q24(zc), (uint32_t)q2.w);
-        const bool win = in && zc == zw && k < best;
-        best = win ? k : best;
+    lds_int4v *ve = (lds_int4v *)(ent) + 3 * e;
+    return EntryRegs{ve[0], ve[1], ve[2]};
+}
+
+template <bool NoDepth, bool Large>
+__device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__restrict__ frame_recs, short2v pix,
+                                             float2v pxy, int i, int j, uint64_t &best)
+{
+    bool in;
+    if (!Large) {
+        // R3 on tile-relative exact int32 values: E + owned > 0 for all three edges
+        // (scalars first: clang's __builtin_bit_cast of an ext_vector component reads component 0)
+        const int ab0 = q.q0.w, ab1 = q.q1.x, ab2 = q.q1.y;
+        const int e0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab0), pix, q.q0.x, false);
+        const int e1 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab1), pix, q.q0.y, false);
+        const int e2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, ab2), pix, q.q0.z, false);
+        in = min(e0, min(e1, e2)) > 0;
+    } else {
+        const Rec &r = frame_recs[__builtin_amdgcn_readfirstlane(q.q0.x)];
+        int64_t E[3];
+        edge_values(r, i, j, E);
+        in = inside(r, E);
     }
+    // R4 without branches: in range iff the clamp leaves zw unchanged (false for NaN)
+    const float2v d = pxy - float2v{__int_as_float(q.q2.x), __int_as_float(q.q2.y)};
+    const float zw = depth_at(__int_as_float(q.q1.z), __int_as_float(q.q1.w), __int_as_float(q.q2.z), d.x, d.y);
+    const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
+    const uint64_t k = depth_key<NoDepth>(depth_q24(zc), (uint32_t)q.q2.w);
+    const bool win = in && zc == zw && k < best;
+    best = win ? k : best;
 }
 
 // per-workgroup phase timestamps of the instrumented backward (AB & 128, dirt_debug_bwd_variant 128)
@@ -689,14 +689,31 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
                                                        const Rec *frame_recs, const FaceData *fdata_frame, int F, int f,
                                                        int i, int j)
 {
+    // int32 when every lane's |E| < 2^30 and |A|, |B| < 2^22 (a one-pixel step stays inside int32)
+    bool small = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        small = small && E[k] > -(1ll << 30) && E[k] < (1ll << 30) && r.A[k] > -(1 << 22) && r.A[k] < (1 << 22) &&
+                r.B[k] > -(1 << 22) && r.B[k] < (1 << 22);
+    const bool all_small = __builtin_amdgcn_ballot_w64(!small) == 0;
+    int32_t eo[3];  // E + owned
+#pragma unroll
+    for (int k = 0; k < 3; ++k) eo[k] = (int32_t)E[k] + ((r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0)) ? 1 : 0);
     uint32_t bits = 0;
 #pragma unroll
     for (int dir = 0; dir < 4; ++dir) {
         const int axis = dir >> 1, sg = (dir & 1) ? -1 : 1;
-        int64_t Eq[3];
+        bool c;
+        if (all_small) {
+            c = true;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) Eq[k] = E[k] + (int64_t)(axis == 0 ? r.A[k] : r.B[k]) * (256 * sg);
-        bool c = inside(r, Eq);
+            for (int k = 0; k < 3; ++k) c = c && eo[k] + (axis == 0 ? r.A[k] : r.B[k]) * (256 * sg) > 0;
+        } else {
+            int64_t Eq[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) Eq[k] = E[k] + (int64_t)(axis == 0 ? r.A[k] : r.B[k]) * (256 * sg);
+            c = inside(r, Eq);
+        }
         if (!c && multi) c = covers_face_multi(ri, frame_recs, fdata_frame, F, f, i + (axis == 0 ? sg : 0), j + (axis == 1 ? sg : 0));
         bits |= (c ? 1u : 0u) << dir;
     }
@@ -705,8 +722,11 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
 
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
+#ifndef DIRT_RASTER_WAVES
+#define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow
+#endif
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
-__global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
+__global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      uint32_t *__restrict__ zcounts, int64_t nzcounts,
                                                      const uint64_t *__restrict__ coffset,
@@ -739,8 +759,10 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     }
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     const int C = CC > 0 ? CC : Cdyn;
-    __shared__ int32_t s_list_all[kStrips][kListCap];
-    __shared__ StripEntry s_ent_all[kStrips][64];
+    __shared__ int32_t t_list[kStrips][kFilterBlock];  // per-wave segments of the tile's survivors
+    __shared__ int32_t t_nw[2][kStrips];                // segment lengths, double-buffered by chunk parity
+    __shared__ StripEntry t_ent[256];                   // one staging round: an entry per thread
+    __shared__ uint8_t t_mask[256];                     // strips the entry can cover; bit 4: large
     // Gouraud: XCD bands (L2 sharing of bins / records between neighbouring tiles); a procedural
     // program is compute-bound and its cost follows the image content (sky vs water), so its tiles are
     // interleaved over the XCDs instead (round-robin dispatch order) for balance
@@ -748,10 +770,8 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     const int tx = tile % ntx, ty = tile / ntx;
     const int t = threadIdx.x, lx = t & 15, ly = t >> 4, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    int32_t *s_list = s_list_all[wave];
-    StripEntry *s_ent = s_ent_all[wave];
     const int i = tx * kTile + lx, j = ty * kTile + ly;
-    const int dx = lx * 256, dy = (ly & 3) * 256;
+    const int dx = lx * 256, dy = ly * 256;  // offset from the tile origin (sub-pixels)
     const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const bool in_frame = i < W && j < H;
@@ -766,76 +786,120 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     }
 
     uint64_t best = kKeyInit<kNoDepth>;
-    const short2v pix = {(short)dx, (short)dy};  // lane offset from the strip origin in sub-pixels
+    const short2v pix = {(short)dx, (short)dy};  // lane offset from the tile origin in sub-pixels
     const float2v pxy = {fxl, fyl};
-    const int si0 = tx * kTile, sj0 = ty * kTile + wave * 4;
-    const int cx = si0 >> cshift, cy = sj0 >> cshift;
+    const int ti0 = tx * kTile, tj0 = ty * kTile;
+    const int cx = ti0 >> cshift, cy = tj0 >> cshift;
     const int c = cy * nctx + cx;
     const int64_t cc = (int64_t)b * (ncoarse + 1) + c;
     const uint64_t off = coffset[cc];
     const uint32_t cnt = (uint32_t)(coffset[cc + 1] - off);
-    // strip rectangle relative to the coarse tile
-    const uint32_t rx0 = (uint32_t)(si0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
-    const uint32_t ry0 = (uint32_t)(sj0 - (cy << cshift)), ry1 = ry0 + 3;
+    // tile rectangle relative to the coarse tile
+    const uint32_t rx0 = (uint32_t)(ti0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
+    const uint32_t ry0 = (uint32_t)(tj0 - (cy << cshift)), ry1 = ry0 + kTile - 1;
 
     if (AB & 8) {
         best = cnt + off;
     } else if (off + cnt <= (uint64_t)(b + 1) * (uint64_t)frame_capacity) {
-        int n_s = 0;
-        for (uint32_t blk = 0;; blk += kFilterBlock) {
-            const bool more = blk < cnt;
-            if (more) {
-                // a. filter the coarse bin (independent loads per lane in flight)
-                constexpr int U = kFilterBlock / 64;
-                uint2 ev[U];
-                bool ok[U];
+        // The workgroup reads its coarse bin once: each wave filters a quarter of every 512-entry chunk
+        // against the tile into its own list segment; the tile's survivors are staged once (an entry per
+        // thread, with the mask of strips it can cover) and every wave rasterises the entries that reach
+        // its strip.  Chunks and rounds are workgroup-uniform, so every thread meets every barrier.
+        int par = 0;
+        for (uint32_t chunk = 0; chunk < cnt; chunk += kStrips * kFilterBlock, par ^= 1) {
+            constexpr int U = kFilterBlock / 64;
+            uint2 ev[U];
+            bool ok[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t idx = blk + u * 64 + lane;
-                    ok[u] = idx < cnt;
-                    ev[u] = ok[u] ? bins[off + idx] : make_uint2(0u, 0u);
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t bb = ev[u].y;
-                    const bool keep = ok[u] && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 &&
-                                      ((bb >> 16) & 0xff) <= ry1 && (bb >> 24) >= ry0;
-                    const uint64_t mask = __ballot(keep);
-                    if (keep) {
-                        const int pos = n_s + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                        s_list[pos] = (int32_t)ev[u].x;
-                    }
-                    n_s += __popcll(mask);
-                }
+            for (int u = 0; u < U; ++u) {
+                const uint32_t idx = chunk + wave * kFilterBlock + u * 64 + lane;
+                ok[u] = idx < cnt;
+                ev[u] = ok[u] ? bins[off + idx] : make_uint2(0u, 0u);
             }
-            if (n_s == 0 && !more) break;
-            if (n_s < kListCap - kFilterBlock && more) continue;
-            wave_lds_sync();
+            int n_w = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t bb = ev[u].y;
+                const bool keep = ok[u] && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 &&
+                                  ((bb >> 16) & 0xff) <= ry1 && (bb >> 24) >= ry0;
+                const uint64_t mask = __ballot(keep);
+                if (keep)
+                    t_list[wave][n_w + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] =
+                        (int32_t)ev[u].x;
+                n_w += __popcll(mask);
+            }
+            if (lane == 0) t_nw[par][wave] = n_w;
+            __syncthreads();
+            int pre[kStrips + 1];
+            pre[0] = 0;
+#pragma unroll
+            for (int w = 0; w < kStrips; ++w) pre[w + 1] = pre[w] + t_nw[par][w];
+            const int n_list = pre[kStrips];
             if (AB & 2) {
-                best += (uint64_t)(s_list[lane & (kListCap - 1)] + n_s);
-                n_s = 0;
-                if (!more) break;
+                best += (uint64_t)n_list;
+                __syncthreads();
                 continue;
             }
-            // b + c: stage and rasterise the collected survivors, 64 at a time
-            for (int from = 0; from < n_s; from += 64) {
-                const int m = min(64, n_s - from);
-                bool large;
-                const int ne = stage_strip(frame_recs, s_list, from, m, si0, sj0, F, s_ent, lane, large);
-                wave_lds_sync();
-                if (AB & 1) {
-                    if (ne > 0) best += s_ent[lane % ne].key;
-                    wave_lds_sync();
-                    continue;
+            for (int from = 0; from < n_list; from += 256) {
+                const int g = from + t;
+                uint32_t m = 0;
+                if (g < n_list) {
+                    int w = 0;
+#pragma unroll
+                    for (int q = 1; q < kStrips; ++q) w += g >= pre[q] ? 1 : 0;
+                    const int32_t ri = t_list[w][g - pre[w]];
+                    StripEntry E;
+                    bool large;
+                    m = stage_tile(frame_recs, ri, ti0, tj0, F, E, large);
+                    int4 *d = reinterpret_cast<int4 *>(&t_ent[t]);
+                    d[0] = make_int4(E.e[0], E.e[1], E.e[2], (int)E.ab[0]);
+                    d[1] = make_int4((int)E.ab[1], (int)E.ab[2], __float_as_int(E.za), __float_as_int(E.zb));
+                    d[2] = make_int4(__float_as_int(E.fx0), __float_as_int(E.fy0), __float_as_int(E.z0), (int)E.key);
+                    m |= large ? 16u : 0u;
                 }
-                const int4 *ent4 = reinterpret_cast<const int4 *>(s_ent);
-                if (large) raster_entries<kNoDepth, true>(ent4, ne, frame_recs, pix, pxy, i, j, best);
-                else raster_entries<kNoDepth, false>(ent4, ne, frame_recs, pix, pxy, i, j, best);
-                wave_lds_sync();
+                t_mask[t] = (uint8_t)m;
+                __syncthreads();
+                const int nst = min(256, n_list - from);
+                if (!(AB & 1)) {
+                    for (int c0 = 0; c0 < nst; c0 += 64) {
+                        const uint32_t mm = c0 + lane < nst ? t_mask[c0 + lane] : 0u;
+                        uint64_t mine = __ballot((mm >> wave) & 1u);
+                        const uint64_t big = __ballot((mm >> 4) & 1u) & mine;
+                        if (big == 0) {
+                            // two entries per iteration: both sets of reads in flight before either test
+                            while (mine) {
+                                const int e0 = c0 + (int)__builtin_ctzll(mine);
+                                mine &= mine - 1;
+                                if (mine) {
+                                    const int e1 = c0 + (int)__builtin_ctzll(mine);
+                                    mine &= mine - 1;
+                                    const EntryRegs qa = load_entry(t_ent, e0), qb = load_entry(t_ent, e1);
+                                    raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, i, j, best);
+                                    raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, i, j, best);
+                                } else {
+                                    raster_entry<kNoDepth, false>(load_entry(t_ent, e0), frame_recs, pix, pxy, i, j, best);
+                                }
+                            }
+                        } else {
+                            while (mine) {
+                                const int bit = (int)__builtin_ctzll(mine);
+                                mine &= mine - 1;
+                                const EntryRegs q = load_entry(t_ent, c0 + bit);
+                                if ((big >> bit) & 1)
+                                    raster_entry<kNoDepth, true>(q, frame_recs, pix, pxy, i, j, best);
+                                else
+                                    raster_entry<kNoDepth, false>(q, frame_recs, pix, pxy, i, j, best);
+                            }
+                        }
+                    }
+                } else if (nst > 0) {
+                    best += t_ent[lane % nst].key;
+                }
+                // t_ent / t_mask are rewritten by the next round of this chunk; a next chunk rewrites
+                // them only after its own filter barrier, and the last round needs no barrier at all
+                if (from + 256 < n_list) __syncthreads();
             }
-            n_s = 0;
-            if (!more) break;
         }
     } else {
         // bin overflow (capacity too small for this input): test every record of the frame
@@ -873,7 +937,20 @@ __global__ __launch_bounds__(256) void raster_kernel(const float *__restrict__ b
     int64_t E[3];
     edge_values(r, i, j, E);
     float lam[3] = {0.0f, 0.0f, 0.0f};
-    parent_lambda(r, E, lam);
+    // R6 with the int64 -> float conversions done in int32 when every value of the wave fits (the same
+    // integers, so the same floats); non-clipped faces skip the identity basis (m_k >= +0 are exact)
+    bool fits = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fits = fits && E[k] == (int64_t)(int32_t)E[k];
+    float fE[3];
+    if (__builtin_amdgcn_ballot_w64(!fits) == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fE[k] = (float)(int32_t)E[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fE[k] = (float)E[k];
+    }
+    parent_lambda_f(r, fE, fd.clipped == 0, lam);
     if constexpr (SH == DIRT_SHADER_OCEANIC_HORIZON) {
         // texCoordV = perspective-correct clip xy (shaders.cpp:19,21 alias texCoord to position); jitter by
         // the background texel at (texCoordV+1)/2 (NEAREST), channels x,y (C=1 broadcast)

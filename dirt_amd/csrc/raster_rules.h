@@ -68,9 +68,10 @@ struct Tri {
     float v[3][4];
 };
 
-__host__ __device__ inline int face_of_record(int64_t ri, int F)
+// record indices are < 6F <= 6 * 2^26 < 2^31: 32-bit arithmetic (a 64-bit division by 5 is ~15 VALU)
+__host__ __device__ inline int face_of_record(int32_t ri, int F)
 {
-    return ri < F ? (int)ri : (int)((ri - F) / kExtraPerFace);
+    return ri < F ? ri : (int)((uint32_t)(ri - F) / (uint32_t)kExtraPerFace);
 }
 
 __host__ __device__ inline int64_t rec_index(int F, int f, int s)
@@ -198,6 +199,24 @@ __device__ __forceinline__ bool parent_lambda(const Rec &r, const int64_t E[3], 
     if (s == 0.0f) return false;
     const float rs = 1.0f / s;
     const float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
+    return true;
+}
+
+// R6 from the edge values already converted to float (fE[k] == (float)E[k]); `identity`: the record's
+// basis is the identity (non-clipped face), where (m0*1 + m1*0) + m2*0 == m0 exactly since m_k >= +0
+__device__ __forceinline__ bool parent_lambda_f(const Rec &r, const float fE[3], bool identity, float lam[3])
+{
+    const float a0 = fE[0] * r.iw[0], a1 = fE[1] * r.iw[1], a2 = fE[2] * r.iw[2];
+    const float s = (a0 + a1) + a2;
+    if (s == 0.0f) return false;
+    const float rs = 1.0f / s;
+    const float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
+    if (identity) {
+        lam[0] = m0; lam[1] = m1; lam[2] = m2;
+        return true;
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
     return true;
