@@ -26,7 +26,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 BWD_ACCUMULATE = 1     # dirt_rasterise_bwd flags
@@ -98,7 +98,7 @@ def workspace_sizes(B, H, W, C, V, F, bin_capacity=0):
     return saved.value, scratch.value
 
 
-NUM_KERNELS = 5
+NUM_KERNELS = 3
 
 
 def profile_enable(on=True):

@@ -59,9 +59,8 @@ int fail(int code, const char *msg)
 
 // ------------------------------------------------------------------------------------------------
 // Optional per-kernel event timing (bench.py roofline); off by default, host-side only.
-enum KernelId { K_SETUP = 0, K_SCAN, K_FILL, K_RASTER, K_GRAD, K_COUNT };
-const char *const kKernelNames[K_COUNT] = {"setup_kernel", "scan_kernel", "fill_kernel", "raster_kernel",
-                                           "grad_kernel"};
+enum KernelId { K_SETUP = 0, K_RASTER, K_GRAD, K_COUNT };
+const char *const kKernelNames[K_COUNT] = {"setup_kernel", "raster_kernel", "grad_kernel"};
 struct Profiler {
     bool enabled = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[K_COUNT];
@@ -88,36 +87,49 @@ struct ProfScope {
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
 // ------------------------------------------------------------------------------------------------
-// Workspace layout.  saved = records [B][6F] (128 B) + FaceData [B][F] (32 B): what the backward reads.
-// scratch = coarse-tile counts, cursors, offsets and the coarse bins (forward only).
+// Workspace layout.  saved = records [B][6F] (128 B) + FaceData [B][F] (32 B) + 4 neighbour-coverage
+// bits per pixel: what the backward reads.  scratch = two sets of per-coarse-tile counts (alternating
+// forwards: see kParP), a flag area, and the coarse bins: one fixed-capacity slab per (frame, coarse tile).
 //
-// Binning is two-level.  Coarse tiles (64x64 px, 128x128 above 4096 px) are binned globally with
-// one device atomic per (workgroup, coarse tile) -- workgroups of 256 faces pre-aggregate in LDS,
-// so the count/fill passes issue ~ncoarse atomics per workgroup instead of one per (face, tile)
-// (scattered device atomics run at ~20 G/s chip-wide on MI355X: 280k of them cost ~14 us).  The
-// fine 16x16-tile / 16x4-strip binning happens inside the raster kernel, per wave, in LDS.
+// Binning is two-level.  Coarse tiles (64x64 px, 128x128 above 4096 px) are binned by the setup kernel
+// itself: each workgroup of 256 faces counts its (record, coarse tile) pairs in LDS, reserves its range
+// of every touched slab with one returning device atomic per (workgroup, coarse tile), and writes the
+// entries -- no separate count/scan/fill passes (a dependent kernel boundary costs ~1.7 us, and the
+// fill pass had to re-read every record).  HBM is plentiful (288 GB), so the default slab holds as many
+// entries as the frame has faces (+25 % for clipped sub-triangles): a tile overflows only under that
+// budget or an explicit small bin_capacity, and an overflowed tile's raster workgroup then filters every
+// record of the frame itself (slow, exact).  The fine 16x16-tile binning happens inside the raster
+// kernel, in LDS.
 struct Layout {
     int ntx, nty, ntiles;     // fine tiles per frame
     int cshift, csize;        // coarse tile edge = 1 << cshift pixels
     int nctx, ncty, ncoarse;  // coarse tiles per frame (<= kMaxCoarse)
     int64_t nrec;
     size_t saved_recs, saved_fdata, saved_cov, saved_total;
-    size_t off_count, off_cursor, off_offset, off_flag, off_bins, scratch_total;
-    int64_t bin_capacity;
-    int64_t frame_capacity;   // bins of frame b: [b * frame_capacity, (b + 1) * frame_capacity)
+    size_t off_count, off_flag, off_bins, scratch_total;
+    int64_t bin_capacity;     // entries in all slabs
+    uint32_t slab;            // entries per (frame, coarse tile) slab
 };
 
-constexpr int kMaxCoarse = 4096;   // LDS histogram size in setup/fill
+constexpr int kMaxCoarse = 4096;   // LDS histogram size in setup
 constexpr int kFacesPerThread = 1;
 constexpr int kBinThreads = 256;
 constexpr int kFacesPerBlock = kFacesPerThread * kBinThreads;
+constexpr int64_t kDefaultBinBudget = 1ll << 27;  // entries (1 GiB) above which the default slab shrinks
+// Count-set parity, so that no kernel has to return the counts it read to zero.  Words of the flag area
+// (separate 64-B lines): [0] out-of-range-face flag, [kParP] P, [kParQ] Q.  The setup kernel reads p = Q,
+// publishes P = p, accumulates into counts[p] and zeroes counts[p ^ 1] (read by the previous forward's
+// raster, which has completed); the raster kernel reads p = P, bins from counts[p] and publishes
+// Q = p ^ 1 for the next forward.  Each word is only read by one kernel and only written (one workgroup,
+// one value) by the other, so no launch reads a word it writes.  Zeroed scratch = a valid state.
+constexpr int kParP = 16, kParQ = 32;
 
 int64_t default_capacity(int B, int F, int ncoarse)
 {
-    int64_t c = 8 * (int64_t)B * (int64_t)F + 4 * (int64_t)B * ncoarse;
-    if (c < (1 << 20)) c = 1 << 20;
-    if (c > 0x7fffffffLL) c = 0x7fffffffLL;
-    return c;
+    const int64_t slabs = (int64_t)B * ncoarse;
+    int64_t per = (int64_t)F + F / 4 + 64;
+    if (slabs * per > kDefaultBinBudget) per = std::max<int64_t>(kDefaultBinBudget / std::max<int64_t>(slabs, 1), 256);
+    return slabs * per;
 }
 
 int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
@@ -131,18 +143,17 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.ncty = (H + L.csize - 1) >> L.cshift;
     L.ncoarse = L.nctx * L.ncty;
     L.nrec = (int64_t)(1 + kExtraPerFace) * F;
-    L.bin_capacity = bin_capacity > 0 ? (bin_capacity > 0x7fffffffLL ? 0x7fffffffLL : bin_capacity)
-                                      : default_capacity(B, F, L.ncoarse);
+    const int64_t slabs = std::max<int64_t>((int64_t)B * L.ncoarse, 1);
+    L.bin_capacity = bin_capacity > 0 ? bin_capacity : default_capacity(B, F, L.ncoarse);
+    L.slab = (uint32_t)std::min<int64_t>(std::max<int64_t>(L.bin_capacity / slabs, 1), 0x7fffffffLL);
+    L.bin_capacity = (int64_t)L.slab * slabs;
     L.saved_recs = 0;
     L.saved_fdata = (size_t)align_up((int64_t)B * L.nrec * (int64_t)sizeof(Rec), 256);
     L.saved_cov = L.saved_fdata + (size_t)align_up((int64_t)B * F * (int64_t)sizeof(FaceData), 256);
     L.saved_total = L.saved_cov + (size_t)align_up((int64_t)B * H * W, 256);  // 4 coverage bits per pixel
     const int64_t nc = (int64_t)B * L.ncoarse;
     size_t o = 0;
-    L.frame_capacity = B > 0 ? L.bin_capacity / B : 0;
-    L.off_count = o;  o += (size_t)align_up(nc * 4, 256);
-    L.off_cursor = o; o += (size_t)align_up(nc * 4, 256);
-    L.off_offset = o; o += (size_t)align_up((nc + B) * 8, 256);  // ncoarse + 1 offsets per frame
+    L.off_count = o;  o += (size_t)align_up(2 * nc * 4, 256);  // counts[2][B][ncoarse]
     L.off_flag = o;   o += 256;
     L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 8, 256);
     L.scratch_total = o;
@@ -303,15 +314,38 @@ __device__ __forceinline__ void coarse_pairs_flush(BigQueue &Q, Op op)
     __syncthreads();
 }
 
+__device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, int cy, int cshift)
+{
+    const int lim = (1 << cshift) - 1;
+    const int ox = cx << cshift, oy = cy << cshift;
+    const int a0 = max((int)(bx & 0xffff) - ox, 0), a1 = min((int)(bx >> 16) - ox, lim);
+    const int b0 = max((int)(by & 0xffff) - oy, 0), b1 = min((int)(by >> 16) - oy, lim);
+    return (uint32_t)a0 | ((uint32_t)a1 << 8) | ((uint32_t)b0 << 16) | ((uint32_t)b1 << 24);
+}
+
+// K1: setup + coarse binning.  Bin entry = {record index, bbox clamped to the coarse tile, 8 bits per
+// side}; order inside a slab is irrelevant (the depth resolve is a commutative min).
 __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restrict__ verts,
                                                             const int32_t *__restrict__ faces, int V, int F, int W,
                                                             int H, int cshift, int nctx, int ncoarse, int64_t nrec,
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
-                                                            uint32_t *__restrict__ ccount, uint32_t *__restrict__ flag)
+                                                            uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
+                                                            uint2 *__restrict__ bins, uint32_t slab, int B)
 {
     __shared__ uint32_t hist[kMaxCoarse];
+    __shared__ uint32_t base[kMaxCoarse];
     __shared__ BigQueue Q;
     const int b = blockIdx.y, t = threadIdx.x;
+    const int64_t ncount = (int64_t)B * ncoarse;
+    const uint32_t par = flag[kParQ] & 1u;
+    uint32_t *ccount = counts + par * ncount;
+    {
+        // publish this forward's parity for the raster; zero the other count set for the next forward
+        const int64_t g = (int64_t)blockIdx.y * gridDim.x + blockIdx.x, ng = (int64_t)gridDim.x * gridDim.y;
+        if (g == 0 && t == 0) flag[kParP] = par;
+        uint32_t *other = counts + (par ^ 1u) * ncount;
+        for (int64_t k = g * kBinThreads + t; k < ncount; k += ng * kBinThreads) other[k] = 0;
+    }
     for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
     if (t == 0) Q.n = 0;
     __syncthreads();
@@ -319,9 +353,12 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     Rec *frame_recs = recs + (int64_t)b * nrec;
     const float *vb = verts + (int64_t)b * V * 4;
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
-    for (int q = 0; q < kFacesPerThread; ++q) {
-        const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
-        if (f >= F) break;
+    const int f = blockIdx.x * kFacesPerBlock + t;
+    // what the placement pass needs again: the fast-path record's packed bbox, or the sub-record count
+    int nsub = 0;
+    bool fast = false;
+    uint32_t fbx = 1, fby = 0;
+    if (f < F) {
         const int64_t gid = (int64_t)b * F + f;
         const int32_t i0 = faces[gid * 3], i1 = faces[gid * 3 + 1], i2 = faces[gid * 3 + 2];
         const int32_t vidx[3] = {i0, i1, i2};
@@ -347,8 +384,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         fd.clipped = 0;
         Rec r;
         set_empty(r, f);
-        int nsub = 0;
-        bool fast = ok;
+        fast = ok;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const float w = tri.v[k][3];
@@ -359,8 +395,9 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
             make_record(tri.v, id, W, H, f, r);
             nsub = 1;
             frame_recs[f] = r;
-            coarse_pairs_add(Q, f, (uint32_t)r.i0 | ((uint32_t)r.i1 << 16), (uint32_t)r.j0 | ((uint32_t)r.j1 << 16),
-                             cshift, count);
+            fbx = (uint32_t)r.i0 | ((uint32_t)r.i1 << 16);
+            fby = (uint32_t)r.j0 | ((uint32_t)r.j1 << 16);
+            coarse_pairs_add(Q, f, fbx, fby, cshift, count);
         } else {
             frame_recs[f] = r;  // empty unless clip_face overwrites it
 #ifndef DIRT_SETUP_NO_CLIP
@@ -380,110 +417,27 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         fdata[gid] = fd;
     }
     coarse_pairs_flush<kBinThreads>(Q, count);
-    // one device atomic per touched (workgroup, coarse tile), without return: nothing in this launch
-    // waits for them (a device-scope round trip costs ~2 us); fill reads the totals after the launch
-    // boundary and scans them itself
+    // reserve this workgroup's range of every touched slab: one returning device atomic per (workgroup,
+    // coarse tile), all in flight together
     uint32_t *cc = ccount + (int64_t)b * ncoarse;
-    for (int c = t; c < ncoarse; c += kBinThreads)
-        if (hist[c]) __hip_atomic_fetch_add(&cc[c], hist[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ------------------------------------------------------------------------------------------------
-// K3: fill the coarse bins.  Entry = {record index, bbox clamped to the coarse tile, 8 bits per side}.
-// Pass 1 counts per coarse tile in LDS, one device atomic per touched coarse tile reserves the
-// workgroup's range, pass 2 hands out positions with LDS atomics.  Order inside a bin is irrelevant
-// (the depth resolve is a commutative min).
-
-__device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, int cy, int cshift)
-{
-    const int lim = (1 << cshift) - 1;
-    const int ox = cx << cshift, oy = cy << cshift;
-    const int a0 = max((int)(bx & 0xffff) - ox, 0), a1 = min((int)(bx >> 16) - ox, lim);
-    const int b0 = max((int)(by & 0xffff) - oy, 0), b1 = min((int)(by >> 16) - oy, lim);
-    return (uint32_t)a0 | ((uint32_t)a1 << 8) | ((uint32_t)b0 << 16) | ((uint32_t)b1 << 24);
-}
-
-__global__ __launch_bounds__(kBinThreads) void fill_kernel(const Rec *__restrict__ recs,
-                                                           const FaceData *__restrict__ fdata, int F, int cshift,
-                                                           int nctx, int ncoarse, int64_t nrec,
-                                                           const uint32_t *__restrict__ ccount,
-                                                           uint64_t *__restrict__ coffset, uint32_t *__restrict__ ccursor,
-                                                           uint2 *__restrict__ bins, int64_t frame_capacity)
-{
-    extern __shared__ uint64_t fill_lds[];
-    uint64_t *base = fill_lds;                                                    // [ncoarse + 1]
-    uint32_t *hist = reinterpret_cast<uint32_t *>(fill_lds + ncoarse + 1);        // [ncoarse]
-    __shared__ uint64_t wave_sums[kBinThreads / 64];
-    __shared__ BigQueue Q;
-    const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t cb = (int64_t)b * ncoarse;
-    const uint64_t fbase = (uint64_t)b * (uint64_t)frame_capacity, fend = fbase + (uint64_t)frame_capacity;
-    // 1. the frame's bin offsets: exclusive scan of setup's per-tile totals, in every workgroup (a few
-    //    hundred L2-resident words; cheaper than a dependent scan launch or a device-wide ticket)
-    {
-        const int per = (ncoarse + kBinThreads - 1) / kBinThreads, k0 = t * per, k1 = min(k0 + per, ncoarse);
-        uint64_t local = 0;
-        for (int k = k0; k < k1; ++k) {
-            const uint32_t v = ccount[cb + k];
-            hist[k] = v;
-            local += v;
-        }
-        uint64_t x = local;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) wave_sums[wave] = x;
-        __syncthreads();
-        uint64_t run = fbase + (x - local);
-        for (int w = 0; w < wave; ++w) run += wave_sums[w];
-        for (int k = k0; k < k1; ++k) {
-            base[k] = run;
-            run += hist[k];
-        }
-        if (t == kBinThreads - 1) base[ncoarse] = run;  // the last thread owns the last (possibly empty) chunk
-        __syncthreads();
-        // the raster reads the offsets from memory (ncoarse + 1 per frame)
-        if (blockIdx.x == 0)
-            for (int k = t; k <= ncoarse; k += kBinThreads) coffset[(int64_t)b * (ncoarse + 1) + k] = base[k];
-        for (int k = t; k < ncoarse; k += kBinThreads) hist[k] = 0;
-        if (t == 0) Q.n = 0;
-        __syncthreads();
-    }
-    // 2. count this workgroup's pairs per coarse tile, reserve its range of each bin, place
-    const Rec *frame_recs = recs + (int64_t)b * nrec;
-    int nsub[kFacesPerThread];
-    auto count = [&](int32_t, uint32_t, uint32_t, int cx, int cy) { atomicAdd(&hist[cy * nctx + cx], 1u); };
-    auto place = [&](int32_t ri, uint32_t bx, uint32_t by, int cx, int cy) {
-        const int c = cy * nctx + cx;
-        const uint64_t dst = base[c] + atomicAdd(&hist[c], 1u);
-        if (dst < fend) bins[dst] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
-    };
-#pragma unroll
-    for (int q = 0; q < kFacesPerThread; ++q) {
-        const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
-        nsub[q] = f < F ? fdata[(int64_t)b * F + f].nsub : 0;
-        for (int s = 0; s < nsub[q]; ++s) {
-            const int64_t ri = rec_index(F, f, s);
-            uint32_t bx, by;
-            load_bbox(frame_recs[ri], bx, by);
-            coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, count);
-        }
-    }
-    coarse_pairs_flush<kBinThreads>(Q, count);
     for (int c = t; c < ncoarse; c += kBinThreads) {
         const uint32_t n = hist[c];
-        if (n) base[c] += atomicAdd(&ccursor[cb + c], n);
+        base[c] = n ? atomicAdd(&cc[c], n) : 0u;
         hist[c] = 0;
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kFacesPerThread; ++q) {
-        const int f = blockIdx.x * kFacesPerBlock + q * kBinThreads + t;
-        for (int s = 0; s < nsub[q]; ++s) {
-            const int64_t ri = rec_index(F, f, s);
+    uint2 *fb = bins + (int64_t)b * ncoarse * slab;
+    auto place = [&](int32_t ri, uint32_t bx, uint32_t by, int cx, int cy) {
+        const int c = cy * nctx + cx;
+        const uint32_t pos = base[c] + atomicAdd(&hist[c], 1u);
+        if (pos < slab) fb[(int64_t)c * slab + pos] = make_uint2((uint32_t)ri, rel_bbox(bx, by, cx, cy, cshift));
+    };
+    if (fast) {
+        coarse_pairs_add(Q, f, fbx, fby, cshift, place);
+    } else {
+        for (int s = 0; s < nsub; ++s) {
             uint32_t bx, by;
+            const int64_t ri = rec_index(F, f, s);
             load_bbox(frame_recs[ri], bx, by);
             coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, place);
         }
@@ -728,9 +682,8 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
 __global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
-                                                     uint32_t *__restrict__ zcounts, int64_t nzcounts,
-                                                     const uint64_t *__restrict__ coffset,
-                                                     const uint2 *__restrict__ bins, int64_t frame_capacity,
+                                                     const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
+                                                     const uint2 *__restrict__ bins, uint32_t slab,
                                                      int B, int H, int W, int Cdyn, int V, int F, int ntx, int cshift,
                                                      int nctx, int ncoarse, int64_t nrec, float *__restrict__ pixels,
                                                      int32_t *__restrict__ gbuffer, uint8_t *__restrict__ covbits,
@@ -741,12 +694,10 @@ __global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const fl
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     if (!(AB & 16)) {
-        // housekeeping spread over all blocks (a few KB each): return setup's bin counts and fill's
-        // cursors to zero for the next forward, and zero-fill the caller's gradient accumulators if it
-        // passed them
+        // housekeeping spread over all blocks (a few KB each): zero-fill the caller's gradient
+        // accumulators if it passed them (the bin counts are returned to zero by their last reader)
         const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
         const int64_t gt = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x, gs = nblk * 256;
-        for (int64_t k = gt; k < nzcounts; k += gs) zcounts[k] = 0;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (zero_a) {
             for (int64_t k = gt; k < (nzero_a >> 2); k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
@@ -791,42 +742,64 @@ __global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const fl
     const int ti0 = tx * kTile, tj0 = ty * kTile;
     const int cx = ti0 >> cshift, cy = tj0 >> cshift;
     const int c = cy * nctx + cx;
-    const int64_t cc = (int64_t)b * (ncoarse + 1) + c;
-    const uint64_t off = coffset[cc];
-    const uint32_t cnt = (uint32_t)(coffset[cc + 1] - off);
+    const int64_t cc = (int64_t)b * ncoarse + c;
+    const uint32_t par = flag[kParP] & 1u;
+    const uint32_t raw = F > 0 ? counts[par * (int64_t)B * ncoarse + cc] : 0u;  // F == 0: setup did not run
+    if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = par ^ 1u;
+    // an overflowed slab (more pairs than its capacity): filter every record of the frame instead
+    const bool overflow = raw > slab;
+    const uint32_t n_items = overflow ? (uint32_t)nrec : raw;
+    const uint2 *slab_bins = bins + cc * slab;
+    const FaceData *fdata_frame = fdata + (int64_t)b * F;
     // tile rectangle relative to the coarse tile
     const uint32_t rx0 = (uint32_t)(ti0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
     const uint32_t ry0 = (uint32_t)(tj0 - (cy << cshift)), ry1 = ry0 + kTile - 1;
 
     if (AB & 8) {
-        best = cnt + off;
-    } else if (off + cnt <= (uint64_t)(b + 1) * (uint64_t)frame_capacity) {
+        best = raw;
+    } else {
         // The workgroup reads its coarse bin once: each wave filters a quarter of every 512-entry chunk
         // against the tile into its own list segment; the tile's survivors are staged once (an entry per
         // thread, with the mask of strips it can cover) and every wave rasterises the entries that reach
         // its strip.  Chunks and rounds are workgroup-uniform, so every thread meets every barrier.
         int par = 0;
-        for (uint32_t chunk = 0; chunk < cnt; chunk += kStrips * kFilterBlock, par ^= 1) {
+        for (uint32_t chunk = 0; chunk < n_items; chunk += kStrips * kFilterBlock, par ^= 1) {
             constexpr int U = kFilterBlock / 64;
-            uint2 ev[U];
-            bool ok[U];
+            uint32_t rid[U];
+            bool keep_u[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t idx = chunk + wave * kFilterBlock + u * 64 + lane;
-                ok[u] = idx < cnt;
-                ev[u] = ok[u] ? bins[off + idx] : make_uint2(0u, 0u);
+                const bool ok = idx < n_items;
+                if (!overflow) {
+                    const uint2 ev = ok ? slab_bins[idx] : make_uint2(0u, 0u);
+                    const uint32_t bb = ev.y;
+                    rid[u] = ev.x;
+                    keep_u[u] = ok && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 && ((bb >> 16) & 0xff) <= ry1 &&
+                                (bb >> 24) >= ry0;
+                } else {
+                    // record slot idx: sub-triangle 0 of face idx, or slot F + 5f + s - 1 (valid if s < nsub)
+                    bool valid = ok;
+                    if (valid && idx >= (uint32_t)F) {
+                        const uint32_t d = idx - (uint32_t)F, fq = d / kExtraPerFace;
+                        valid = fdata_frame[fq].nsub > (int)(d - fq * kExtraPerFace + 1);
+                    }
+                    uint32_t bx = 1, by = 0;
+                    if (valid) load_bbox(frame_recs[idx], bx, by);
+                    rid[u] = idx;
+                    keep_u[u] = valid && (bx & 0xffff) <= (bx >> 16) && (int)(bx & 0xffff) <= ti0 + kTile - 1 &&
+                                (int)(bx >> 16) >= ti0 && (int)(by & 0xffff) <= tj0 + kTile - 1 && (int)(by >> 16) >= tj0;
+                }
             }
             int n_w = 0;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t bb = ev[u].y;
-                const bool keep = ok[u] && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 &&
-                                  ((bb >> 16) & 0xff) <= ry1 && (bb >> 24) >= ry0;
+                const bool keep = keep_u[u];
                 const uint64_t mask = __ballot(keep);
                 if (keep)
                     t_list[wave][n_w + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] =
-                        (int32_t)ev[u].x;
+                        (int32_t)rid[u];
                 n_w += __popcll(mask);
             }
             if (lane == 0) t_nw[par][wave] = n_w;
@@ -901,21 +874,7 @@ __global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const fl
                 if (from + 256 < n_list) __syncthreads();
             }
         }
-    } else {
-        // bin overflow (capacity too small for this input): test every record of the frame
-        for (int f = 0; f < F; ++f) {
-            const int ns = fdata[(int64_t)b * F + f].nsub;
-            for (int s = 0; s < ns; ++s) {
-                const int64_t ri = rec_index(F, f, s);
-                const Rec &r = frame_recs[ri];
-                if (r.i0 > r.i1) continue;
-                int64_t E[3];
-                edge_values(r, i, j, E);
-                depth_update<kNoDepth>(r, ((uint32_t)f << 3) | (uint32_t)s, fxl, fyl, inside(r, E), best);
-            }
-        }
     }
-
     if (!in_frame) return;
     float *out = pixels + o * C;
     if (AB & 15) {
@@ -1671,7 +1630,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 4; }
+int dirt_abi_version(void) { return 5; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -1721,35 +1680,25 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
     uint8_t *covbits = reinterpret_cast<uint8_t *>(sv + L.saved_cov);
     uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
-    uint32_t *ccursor = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_cursor);
-    uint64_t *coffset = reinterpret_cast<uint64_t *>(sc + L.off_offset);
     uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
     uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
-    const int64_t nzcounts = (int64_t)((L.off_offset - L.off_count) / 4);
 
-    // counts and cursors are adjacent: one memset, unless the caller vouches that they are zero
-    // (DIRT_FWD_SCRATCH_CLEAN: every forward's raster kernel returns them to zero)
-    if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_offset - L.off_count, stream));
+    // count sets and parity words: one memset, unless the caller vouches that the scratch is clean
+    // (DIRT_FWD_SCRATCH_CLEAN: zeroed once and since used only by forwards of the same layout)
+    if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
     const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     if (F > 0) {
-        {
-            ProfScope ps(K_SETUP, stream);
-            setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
-                                                                     L.ncoarse, L.nrec, recs, fdata, ccount, flag);
-            HIP_TRY(hipGetLastError());
-        }
-        ProfScope ps(K_FILL, stream);
-        fill_kernel<<<bin_grid, dim3(kBinThreads), (size_t)L.ncoarse * 12 + 8, stream>>>(
-            recs, fdata, F, L.cshift, L.nctx, L.ncoarse, L.nrec, ccount, coffset, ccursor, bins, L.frame_capacity);
+        ProfScope ps(K_SETUP, stream);
+        setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
+                                                                 L.slab, B);
         HIP_TRY(hipGetLastError());
-    } else {
-        HIP_TRY(hipMemsetAsync(coffset, 0, (size_t)(B * (int64_t)(L.ncoarse + 1)) * 8, stream));  // every bin empty
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
 #define LAUNCH_PROC(CC, SHT)                                                                                     \
     raster_kernel<CC, 0, SHT><<<grid, dim3(256), 0, stream>>>(                                                   \
-        background, vertex_colors, recs, fdata, ccount, nzcounts, coffset, bins, L.frame_capacity, B, H, W, C, V, F,\
+        background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F,                     \
         L.ntx,                                                                                                     \
         L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                         \
         zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                      \
@@ -1762,8 +1711,8 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     else if (shader_id >= DIRT_SHADER_OCEANIC)                                                                   \
         LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC);                                                                    \
     else                                                                                                         \
-    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, nzcounts,   \
-                                                      coffset, bins, L.frame_capacity, B, H, W, C, V, F, L.ntx,   \
+    raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, flag,       \
+                                                      bins, L.slab, B, H, W, C, V, F, L.ntx,                     \
                                                       L.cshift,                                                  \
                                                       L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits,          \
                                                       zero_grad_vertices,                                          \
@@ -1855,23 +1804,29 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
 
 // Ablation entry point (tools/ablate.py): re-runs raster_kernel (C == 3) on the bins a preceding
 // dirt_rasterise_fwd left in `scratch`, with parts switched off; returns the kernel time in ms.
-int dirt_debug_raster_variant(int variant, const float *background, const float *vertex_colors, int B, int H, int W,
-                              int C, int V, int F, float *pixels, int32_t *gbuffer, const void *saved,
-                              const void *scratch, void *stream_, float *ms)
+int dirt_debug_raster_variant(int variant, const float *background, const float *vertices, const float *vertex_colors,
+                              const int32_t *faces, int B, int H, int W, int C, int V, int F, float *pixels,
+                              int32_t *gbuffer, void *saved, void *scratch, void *stream_, float *ms)
 {
     if (C != 3) return fail(DIRT_EINVAL, "dirt_debug_raster_variant: C must be 3");
     Layout L;
     int rc = make_layout(B, H, W, F, 0, L);
     if (rc) return rc;
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
-    const char *sv = static_cast<const char *>(saved), *sc = static_cast<const char *>(scratch);
-    const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
-    const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
-    uint8_t *covbits = reinterpret_cast<uint8_t *>(const_cast<char *>(sv) + L.saved_cov);
-    uint32_t *zc = reinterpret_cast<uint32_t *>(const_cast<char *>(sc) + L.off_count);
-    const int64_t nz = (int64_t)((L.off_offset - L.off_count) / 4);
-    const uint64_t *coffset = reinterpret_cast<const uint64_t *>(sc + L.off_offset);
-    const uint2 *bins = reinterpret_cast<const uint2 *>(sc + L.off_bins);
+    char *sv = static_cast<char *>(saved), *sc = static_cast<char *>(scratch);
+    Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
+    FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
+    uint8_t *covbits = reinterpret_cast<uint8_t *>(sv + L.saved_cov);
+    uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
+    uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
+    // re-bin from a clean scratch, then time the raster variant alone
+    HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
+    const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
+    if (F > 0)
+        setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
+                                                                 L.slab, B);
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -1879,8 +1834,8 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
 #define V_RAST(AB)                                                                                                 \
     case AB:                                                                                                       \
-        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, zc, nz, coffset, \
-                                                             bins, L.frame_capacity, B, H, W, C, V, F, L.ntx, L.cshift,\
+        raster_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, flag,    \
+                                                             bins, L.slab, B, H, W, C, V, F, L.ntx, L.cshift,         \
                                                              L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits,     \
                                                              nullptr, 0,                                              \
                                                              nullptr, 0, nullptr, nullptr, 0, C);                    \
@@ -2008,7 +1963,7 @@ int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *s
     if (!scratch || scratch_bytes < L.scratch_total)
         return fail(DIRT_EINVAL, "dirt_scratch_clear: scratch smaller than dirt_workspace_sizes()");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
-    HIP_TRY(hipMemsetAsync(static_cast<char *>(scratch) + L.off_count, 0, L.off_offset - L.off_count, stream));
+    HIP_TRY(hipMemsetAsync(static_cast<char *>(scratch) + L.off_count, 0, L.off_bins - L.off_count, stream));
     return DIRT_OK;
 }
 

@@ -66,11 +66,15 @@ extern "C" {
 #define DIRT_SHADER_HILL 7 /* csrc/shaders.cpp:123-554 (`Hill`, csrc/hill.cpp; camera_pos: 12 floats); no depth
                               test (last face wins), background = terrain lookup, uncovered pixels 0 */
 
-/* ABI version, bumped on any signature change (4: + dirt_hill_fwd, shader ids 6 and 7) */
+/* ABI version, bumped on any signature or workspace-layout change (4: + dirt_hill_fwd, shader ids 6 and 7;
+ * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
- * bin_capacity = number of (tile, triangle) bin entries the scratch can hold (<=0: default policy). */
+ * bin_capacity = number of (coarse tile, triangle) bin entries the scratch can hold, split evenly into
+ * one slab per (frame, coarse tile); <=0: default policy (F + F/4 + 64 entries per slab, so no slab of
+ * a frame overflows unless many faces are clipped into one tile, up to 2^27 entries in all).  A slab
+ * that overflows is still rendered exactly, by a slow path that filters every record of the frame. */
 int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_capacity,
                          size_t *saved_bytes, size_t *scratch_bytes);
 
@@ -129,7 +133,7 @@ int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, s
  * dirt_profile_enable(1) clears and starts recording, (0) clears and stops.  dirt_profile_read
  * synchronises the recorded events of kernel `kernel_id` (0..DIRT_NUM_KERNELS-1) and returns its name,
  * launch count and summed duration.  Not thread-safe; do not enable during hipGraph capture. */
-#define DIRT_NUM_KERNELS 5
+#define DIRT_NUM_KERNELS 3
 int dirt_profile_enable(int enable);
 int dirt_profile_read(int kernel_id, const char **name, int *launches, double *total_ms);
 

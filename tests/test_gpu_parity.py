@@ -116,6 +116,16 @@ def test_bin_overflow_fallback():
     check_scene(*scenes.random_triangles(F=800, W=128, H=96, radius_px=14.0, seed=4), bin_capacity=64)
 
 
+def test_bin_overflow_some_tiles():
+    # a dense cluster in the bottom-left coarse tile overflows its slab (350+ pairs, slab 250) while the
+    # other three stay within theirs: overflowed and binned tiles in one launch, with clipped faces mixed in
+    bg, v, c, f = scenes.random_triangles(F=600, W=128, H=96, radius_px=6.0, seed=11)
+    v = v.copy()
+    v[:400 * 3, :2] = v[:400 * 3, :2] * 0.3 - 0.6   # 400 faces squeezed into x, y in [-0.9, -0.3]
+    v[400 * 3 + 2, 3] = -0.5                          # one vertex behind the eye: the clipping path
+    check_scene(bg, v, c, f, bin_capacity=1000)
+
+
 def test_degenerate_and_out_of_range_faces():
     bg, v, c, f = scenes.random_triangles(F=200, W=64, H=64, radius_px=10.0, seed=9)
     f = f.copy()

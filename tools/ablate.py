@@ -44,14 +44,15 @@ def main():
     for k, name in NAMES.items():
         print("grad   %-28s median %8.2f us  min %8.2f" % (name, np.median(res[k]), np.min(res[k])))
     rfn = lib.dirt_debug_raster_variant
-    rfn.argtypes = [ctypes.c_int, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, P, ctypes.POINTER(ctypes.c_float)]
+    rfn.argtypes = [ctypes.c_int, P, P, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, P, ctypes.POINTER(ctypes.c_float)]
     rfn.restype = ctypes.c_int
     RN = {0: "full", 1: "no pixel loop, no resolve", 2: "bin filter only, no resolve", 4: "no resolve",
           8: "nothing (housekeeping + bg prefetch + gbuffer write)"}
     rres = {k: [] for k in RN}
     for rnd in range(30):
         for k in RN:
-            _lib.check(rfn(k, t[0].data_ptr(), t[2].data_ptr(), B, H, W, C, V, F, sess.pixels.data_ptr(),
+            _lib.check(rfn(k, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), B, H, W, C, V, F,
+                           sess.pixels.data_ptr(),
                            sess.gbuffer.data_ptr(), sess.saved.data_ptr(), sess.scratch.data_ptr(), stream,
                            ctypes.byref(ms)))
             if rnd >= 3:
