@@ -314,6 +314,24 @@ __device__ __forceinline__ void coarse_pairs_flush(BigQueue &Q, Op op)
     __syncthreads();
 }
 
+// per-workgroup phase timestamps of the instrumented backward (AB & 128, dirt_debug_bwd_variant 128)
+constexpr int kTsMaxWG = 1 << 16;
+constexpr int kTsStride = 13;  // 8 phase timestamps, HW_ID, XCC_ID, 3 inside phase B (wave 0)
+__device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
+#define PHASE_TS(n)                                                                                           \
+    do {                                                                                                      \
+        if ((AB & 128) && threadIdx.x == 0) {                                                                 \
+            const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                              \
+            if (wg_ < kTsMaxWG) {                                                                             \
+                g_phase_ts[wg_ * kTsStride + (n)] = __builtin_amdgcn_s_memtime();                             \
+                if ((n) == 0) {                                                                               \
+                    g_phase_ts[wg_ * kTsStride + 8] = __builtin_amdgcn_s_getreg((4) | (31 << 11));            \
+                    g_phase_ts[wg_ * kTsStride + 9] = __builtin_amdgcn_s_getreg((20) | (31 << 11));           \
+                }                                                                                             \
+            }                                                                                                 \
+        }                                                                                                     \
+    } while (0)
+
 __device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, int cy, int cshift)
 {
     const int lim = (1 << cshift) - 1;
@@ -325,6 +343,8 @@ __device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, i
 
 // K1: setup + coarse binning.  Bin entry = {record index, bbox clamped to the coarse tile, 8 bits per
 // side}; order inside a slab is irrelevant (the depth resolve is a commutative min).
+// AB & 128: per-workgroup phase timestamps (dirt_debug_setup_ts, tools/setup_ts.py)
+template <int AB = 0>
 __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restrict__ verts,
                                                             const int32_t *__restrict__ faces, int V, int F, int W,
                                                             int H, int cshift, int nctx, int ncoarse, int64_t nrec,
@@ -336,6 +356,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     __shared__ uint32_t base[kMaxCoarse];
     __shared__ BigQueue Q;
     const int b = blockIdx.y, t = threadIdx.x;
+    PHASE_TS(0);
     const int64_t ncount = (int64_t)B * ncoarse;
     const uint32_t par = flag[kParQ] & 1u;
     uint32_t *ccount = counts + par * ncount;
@@ -362,21 +383,26 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         const int64_t gid = (int64_t)b * F + f;
         const int32_t i0 = faces[gid * 3], i1 = faces[gid * 3 + 1], i2 = faces[gid * 3 + 2];
         const int32_t vidx[3] = {i0, i1, i2};
+        PHASE_TS(10 + (i0 == 0x7fffffff));
         Tri tri;
         bool ok = true;
+        // the three vertex loads are issued together (clamped indices, no per-vertex branch: one
+        // memory round trip instead of three); out-of-range vertices are replaced afterwards
+        float4 pv[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int32_t vi = vidx[k];
-            if (vi < 0 || vi >= V) {
-                ok = false;
-                tri.v[k][0] = tri.v[k][1] = tri.v[k][2] = 0.0f;
-                tri.v[k][3] = 1.0f;
-            } else {
-                const float4 p = *reinterpret_cast<const float4 *>(vb + (int64_t)vi * 4);
-                tri.v[k][0] = p.x; tri.v[k][1] = p.y; tri.v[k][2] = p.z; tri.v[k][3] = p.w;
-                ok = ok && finite4(tri.v[k]);
-            }
+            const bool in = vi >= 0 && vi < V;
+            pv[k] = V > 0 ? *reinterpret_cast<const float4 *>(vb + (int64_t)(in ? vi : 0) * 4) : make_float4(0.f, 0.f, 0.f, 1.f);
+            if (!in) pv[k] = make_float4(0.f, 0.f, 0.f, 1.f);
+            ok = ok && in;
         }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            tri.v[k][0] = pv[k].x; tri.v[k][1] = pv[k].y; tri.v[k][2] = pv[k].z; tri.v[k][3] = pv[k].w;
+            ok = ok && finite4(tri.v[k]);
+        }
+        PHASE_TS(11 + (tri.v[0][0] == 12345.f));
         if (!(i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V)) atomicOr(flag, 1u);
         FaceData fd;
         fd.v[0] = i0; fd.v[1] = i1; fd.v[2] = i2;
@@ -416,7 +442,9 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         fd.nsub = nsub;
         fdata[gid] = fd;
     }
+    PHASE_TS(1);
     coarse_pairs_flush<kBinThreads>(Q, count);
+    PHASE_TS(2);
     // reserve this workgroup's range of every touched slab: one returning device atomic per (workgroup,
     // coarse tile), all in flight together
     uint32_t *cc = ccount + (int64_t)b * ncoarse;
@@ -426,6 +454,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         hist[c] = 0;
     }
     __syncthreads();
+    PHASE_TS(3);
     uint2 *fb = bins + (int64_t)b * ncoarse * slab;
     auto place = [&](int32_t ri, uint32_t bx, uint32_t by, int cx, int cy) {
         const int c = cy * nctx + cx;
@@ -443,6 +472,11 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         }
     }
     coarse_pairs_flush<kBinThreads>(Q, place);
+    if (AB & 128) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        PHASE_TS(7);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -612,24 +646,6 @@ __device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__re
     const bool win = in && zc == zw && k < best;
     best = win ? k : best;
 }
-
-// per-workgroup phase timestamps of the instrumented backward (AB & 128, dirt_debug_bwd_variant 128)
-constexpr int kTsMaxWG = 1 << 16;
-constexpr int kTsStride = 13;  // 8 phase timestamps, HW_ID, XCC_ID, 3 inside phase B (wave 0)
-__device__ uint64_t g_phase_ts[kTsMaxWG * kTsStride];
-#define PHASE_TS(n)                                                                                           \
-    do {                                                                                                      \
-        if ((AB & 128) && threadIdx.x == 0) {                                                                 \
-            const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                              \
-            if (wg_ < kTsMaxWG) {                                                                             \
-                g_phase_ts[wg_ * kTsStride + (n)] = __builtin_amdgcn_s_memtime();                             \
-                if ((n) == 0) {                                                                               \
-                    g_phase_ts[wg_ * kTsStride + 8] = __builtin_amdgcn_s_getreg((4) | (31 << 11));            \
-                    g_phase_ts[wg_ * kTsStride + 9] = __builtin_amdgcn_s_getreg((20) | (31 << 11));           \
-                }                                                                                             \
-            }                                                                                                 \
-        }                                                                                                     \
-    } while (0)
 
 __device__ __noinline__ bool covers_face_multi(int64_t hint_ri, const Rec *frame_recs, const FaceData *fdata_frame,
                                                int F, int f, int i, int j);
@@ -1689,7 +1705,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     if (F > 0) {
         ProfScope ps(K_SETUP, stream);
-        setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+        setup_kernel<0><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
                                                                  L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
                                                                  L.slab, B);
         HIP_TRY(hipGetLastError());
@@ -1824,7 +1840,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
     const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     if (F > 0)
-        setup_kernel<<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+        setup_kernel<0><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
                                                                  L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
                                                                  L.slab, B);
     hipEvent_t e0, e1;
@@ -1846,6 +1862,39 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
         return fail(DIRT_EINVAL, "dirt_debug_raster_variant: unknown variant");
     }
 #undef V_RAST
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    HIP_TRY(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return DIRT_OK;
+}
+
+// Instrumented setup (tools/setup_ts.py): clean scratch, one setup_kernel<128> launch, its time in ms;
+// per-workgroup phase timestamps land in g_phase_ts (dirt_debug_read_phase_ts).
+int dirt_debug_setup_ts(const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F, void *saved,
+                        void *scratch, void *stream_, float *ms)
+{
+    Layout L;
+    int rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    char *sv = static_cast<char *>(saved), *sc = static_cast<char *>(scratch);
+    Rec *recs = reinterpret_cast<Rec *>(sv + L.saved_recs);
+    FaceData *fdata = reinterpret_cast<FaceData *>(sv + L.saved_fdata);
+    uint32_t *ccount = reinterpret_cast<uint32_t *>(sc + L.off_count);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
+    uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
+    HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
+    const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, stream));
+    setup_kernel<128><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
+                                                                   L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
+                                                                   L.slab, B);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, stream));
     HIP_TRY(hipEventSynchronize(e1));

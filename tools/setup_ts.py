@@ -1,0 +1,62 @@
+"""Per-phase timestamps of the instrumented setup kernel (setup_kernel<128>) at config 3.
+
+Phases per workgroup: record setup (faces + vertices loads, R1-R5, record stores), LDS count flush,
+slab reservation (returning device atomics), placement (LDS cursors + bin stores, drained)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+import scenes  # noqa: E402
+from dirt_amd import _lib  # noqa: E402
+from dirt_amd.session import RasteriseSession  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    bg, v, c, f = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
+    t = [torch.from_numpy(a[None]).to(dev) for a in (bg, v, c, f)]
+    B, H, W, C = t[0].shape
+    V, F = t[1].shape[1], t[3].shape[1]
+    sess = RasteriseSession(B, H, W, C, V, F, device=dev)
+    lib = _lib.load()
+    fn = lib.dirt_debug_setup_ts
+    P = ctypes.c_void_p
+    fn.argtypes = [P, P] + [ctypes.c_int] * 5 + [P, P, P, ctypes.POINTER(ctypes.c_float)]
+    rd = lib.dirt_debug_read_phase_ts
+    rd.argtypes = [P, ctypes.c_int]
+    stream = torch.cuda.current_stream().cuda_stream
+    ms = ctypes.c_float(0)
+    nwg = (F + 255) // 256 * B
+    times = []
+    for _ in range(5):
+        _lib.check(fn(t[1].data_ptr(), t[3].data_ptr(), B, H, W, V, F, sess.saved.data_ptr(), sess.scratch.data_ptr(),
+                      stream, ctypes.byref(ms)))
+        times.append(ms.value * 1e3)
+    print("setup_kernel<128>: " + " ".join("%.2f" % x for x in times) + " us")
+    ts = np.zeros((nwg, 13), np.uint64)
+    _lib.check(rd(ts.ctypes.data, nwg))
+    S = ts[:, [0, 10, 11, 12, 1]].astype(np.int64)
+    ok = (S > 0).all(1)
+    dS = np.diff(S[ok], axis=1)
+    for k, name in enumerate(["start -> faces arrived", "faces -> vertices arrived", "vertices -> record computed",
+                              "record -> phase end (stores issued)"]):
+        print("  thread 0: %-36s median %7.0f  p90 %7.0f ticks" % (name, np.median(dS[:, k]), np.percentile(dS[:, k], 90)))
+    T = ts[:, [0, 1, 2, 3, 7]].astype(np.int64)
+    d = np.diff(T, axis=1)
+    life = T[:, 4] - T[:, 0]
+    tick_us = times[-1] / max(float(np.median(life)), 1.0)
+    names = ["records (loads, R1-R5, stores)", "LDS count flush", "slab reservation", "placement (drained)"]
+    for k, name in enumerate(names):
+        print("  %-32s median %7.0f  p90 %7.0f ticks  (%4.1f%% of the median lifetime)" % (
+            name, np.median(d[:, k]), np.percentile(d[:, k], 90), 100.0 * np.median(d[:, k]) / np.median(life)))
+    print("  lifetime median %.0f ticks, p90 %.0f; starts spread %.0f ticks (rebased per XCC)" % (
+        np.median(life), np.percentile(life, 90), np.percentile(T[:, 0] - T[:, 0].min(), 90)))
+
+
+if __name__ == "__main__":
+    main()
