@@ -71,13 +71,29 @@ def cpu_baseline(host, grad_host, budget_s=10.0, max_reps=20):
     while len(times) < max_reps and (time.perf_counter() - t_start < budget_s or len(times) < 1):
         t0 = time.perf_counter()
         px, gb, _ = oracle.rasterise_fwd(bg, v, c, f, nthreads=nthreads)
-        oracle.rasterise_bwd(v, c, f, px, grad_host, gb, nthreads=nthreads)
+        grads = oracle.rasterise_bwd(v, c, f, px, grad_host, gb, nthreads=nthreads)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
     return {"value": B * H * W / t / 1e6, "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
             "sample": "%d x full config frame(s) (%dx%dx%d, F=%d) fwd+bwd, median of %d reps, oracle/dirt_oracle.c "
                       "OpenMP" % (B, H, W, C, f.shape[1], len(times)),
-            "ms_per_frame": t * 1e3 / B}
+            "ms_per_frame": t * 1e3 / B}, (px, gb) + tuple(grads)
+
+
+def parity(sess, ref):
+    """The metric's 'grad max-abs-err vs ref': the benchmarked step's outputs against the CPU oracle on the
+    same frame (forward bit-exact; gradients within the DESIGN.md section 5 tolerance)."""
+    px, gb, rgv, rgc, rgbg = ref
+    out = {"pixels_max_abs_err": float(np.abs(sess.pixels.cpu().numpy() - px).max()),
+           "gbuffer_mismatches": int((sess.gbuffer.cpu().numpy() != gb).sum())}
+    for name, a, b in (("grad_vertices", sess.grad_vertices, rgv), ("grad_vertex_colors", sess.grad_vertex_colors, rgc),
+                       ("grad_background", sess.grad_background, rgbg)):
+        e = np.abs(a.cpu().numpy() - b)
+        out[name + "_max_abs_err"] = float(e.max())
+        out[name + "_max_abs_ref"] = float(np.abs(b).max())
+        tol = 1e-4 * np.abs(b) + 1e-5 * max(float(np.abs(b).max()), 1e-30)
+        out[name + "_within_tol"] = bool((e <= tol).all())
+    return out
 
 
 def main():
@@ -180,9 +196,12 @@ def main():
                 "alg_bytes_per_launch": kbytes[dom], "avg_us": round(kern_us[dom], 2),
                 "op_frac": round((fwd_b + bwd_b) / (ms_per_step * 1e-3 / world) / 1e9 / HBM_PEAK_GBS, 4)}
 
-    cpu = None
+    cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(host, grad_host, budget_s=args.cpu_budget)
+        cpu, ref = cpu_baseline(host, grad_host, budget_s=args.cpu_budget)
+        step()  # one more step so that the session buffers hold this frame's forward and backward
+        torch.cuda.synchronize()
+        par = parity(sess, ref)
 
     if rank == 0:
         out = {
@@ -197,6 +216,7 @@ def main():
                        "hip_graph": not args.no_graph, "steps_per_graph": gs},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity_vs_oracle": par,
             "kernels_us": {k: round(u, 2) for k, u in kern_us.items()},
         }
         print(json.dumps(out))

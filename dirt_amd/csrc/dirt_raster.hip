@@ -693,10 +693,11 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
 #ifndef DIRT_RASTER_WAVES
-#define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow
+#define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
+                             // the procedural programs and the generic-C path keep their natural allocation)
 #endif
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
-__global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
                                                      const uint2 *__restrict__ bins, uint32_t slab,
@@ -744,13 +745,6 @@ __global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const fl
     const bool in_frame = i < W && j < H;
     const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
 
-    // prefetch the background of this pixel (used if nothing covers it; hill's is its terrain texture)
-    float bgv[CM];
-    if (in_frame && !kNoDepth) {
-#pragma unroll
-        for (int c = 0; c < CM; ++c)
-            if (c < C) bgv[c] = background[o * C + c];
-    }
 
     uint64_t best = kKeyInit<kNoDepth>;
     const short2v pix = {(short)dx, (short)dy};  // lane offset from the tile origin in sub-pixels
@@ -903,7 +897,7 @@ __global__ __launch_bounds__(256, DIRT_RASTER_WAVES) void raster_kernel(const fl
         if constexpr (SH == DIRT_SHADER_GOURAUD) covbits[o] = 0;
 #pragma unroll
         for (int c2 = 0; c2 < CM; ++c2)
-            if (c2 < C) out[c2] = kNoDepth ? 0.0f : bgv[c2];
+            if (c2 < C) out[c2] = kNoDepth ? 0.0f : background[o * C + c2];  // (hill: no background copy)
         return;
     }
     const Rec &r = frame_recs[best_rec];
