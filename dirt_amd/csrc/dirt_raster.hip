@@ -1090,6 +1090,7 @@ struct SlotTable {
     uint32_t bx[kSlots], by[kSlots];  // i0 | i1 << 16 (bit 31: large record, use the global Rec)
     int32_t v[3][kSlots];
     float iw[3][kSlots], w[3][kSlots];  // interpolation data of the record (own-pixel path)
+    float h2d[kSlots];                  // 1 / (2 D), D = E0 + E1 + E2 (constant over the plane)
     int32_t n;
 };
 
@@ -1348,6 +1349,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                 T.e[k][sf] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
             }
             T.iw[0][sf] = riw0; T.iw[1][sf] = riw1; T.iw[2][sf] = riw2;
+            T.h2d[sf] = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
             T.bx[sf] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
             T.by[sf] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
         }
@@ -1376,7 +1378,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
         const Rec &rr = frame_recs[rp];  // large records and the basis of clipped faces
         const int hx = lx + 1, hy = ly + 1;  // region coordinates of this pixel
         int32_t mA[3], mB[3], eme[3];       // eme: E + owned here (small records only)
-        float iw0, iw1, iw2, w0, w1, w2;
+        float iw0, iw1, iw2, w0, w1, w2, h2d;
         float fEp[3];
         bool me_small;
         if (sp >= 0) {
@@ -1384,6 +1386,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             for (int k = 0; k < 3; ++k) { mA[k] = T.A[k][sp]; mB[k] = T.B[k][sp]; }
             iw0 = T.iw[0][sp]; iw1 = T.iw[1][sp]; iw2 = T.iw[2][sp];
             w0 = T.w[0][sp]; w1 = T.w[1][sp]; w2 = T.w[2][sp];
+            h2d = T.h2d[sp];
             me_small = !slot_is_large(T, sp);
         } else {
             const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
@@ -1392,6 +1395,9 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
             const FaceData &fdr = fdata_frame[f];
             w0 = fdr.w[0]; w1 = fdr.w[1]; w2 = fdr.w[2];
+            int64_t E0[3];
+            edge_values(me, i, j, E0);
+            h2d = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
             me_small = false;
         }
         if (me_small) {
@@ -1464,20 +1470,31 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                 const float st = (float)(axis == 0 ? mA[k] : mB[k]) * (me_low ? 256.0f : -256.0f);  // = (float)(A * 256)
                 m[k] = (2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2);
             }
-            float lm[3];
-            if (!fast_lambda(rr, multi, m[0], m[1], m[2], lm)) continue;
-            const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
-            if (Wm == 0.0f) continue;
             const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
             const float half = axis == 0 ? ns.half_w : ns.half_h;
             const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
             const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
-            const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
+            float g[3];
+            if (!multi) {
+                // Non-clipped face (identity basis, iw_k w_k = 1): lambda_k / Wm = a_k / sum_k (a_k w_k)
+                // = a_k / (2E_0 + 2E_1 + 2E_2 + st_0 + st_1 + st_2) = a_k / (2D), since the edge
+                // functions sum to the constant D and their steps to 0 -- no division per pair
+                const float c = omega * s * half * h2d;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] = c * m[k];
+            } else {
+                float lm[3];
+                if (!fast_lambda(rr, multi, m[0], m[1], m[2], lm)) continue;
+                const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
+                if (Wm == 0.0f) continue;
+                const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] = tt * lm[k];
+            }
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                const float g = tt * lm[k];
-                acc[k * 3 + axis] += g;
-                acc[k * 3 + 2] -= g * ndc;
+                acc[k * 3 + axis] += g[k];
+                acc[k * 3 + 2] -= g[k] * ndc;
             }
         }
         // colour weights last: keeps their registers out of the pair loop's live range
