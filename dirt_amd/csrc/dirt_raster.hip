@@ -1421,6 +1421,43 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
         // 2 whole); pass 2 interpolates and accumulates.  Splitting keeps the coverage tests' and the
         // accumulators' registers apart (occupancy).
         PHASE_TS(10 + (fEp[0] == 12345.f));
+        if (!(AB & 17) && __builtin_amdgcn_ballot_w64(multi) == 0) {
+            // No clipped face in this wave: ownership and accumulation of the four pairs without
+            // branches (the four directions interleave).  A neighbour shows my face iff it shows my
+            // record (a non-clipped face has exactly one), so no face_of_record per pair.
+            const uint32_t covme = s_cov[kme];
+#pragma unroll
+            for (int dir = 0; dir < 4; ++dir) {
+                const int axis = dir >> 1;
+                const bool me_low = (dir & 1) == 0;
+                const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
+                const int kq = kme + dj * kHalo + di;
+                const int32_t gq = s_gb[kq];
+                const int klo = me_low ? kme : kq;
+                const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
+                const int32_t rq = gq & kGbufIndexMask;
+                const bool mine_covers_other = (covme >> dir) & 1u;
+                const bool other_covers_me = (s_cov[kq] >> (dir ^ 1)) & 1u;
+                // 2: whole, 1: half, 0: none; -2 = outside the frame, -1 = background
+                const uint32_t code = gq == -2 ? 0u
+                                      : gq < 0 ? 2u
+                                      : rq == rp ? (me_low ? 2u : 0u)
+                                      : (!mine_covers_other && other_covers_me) ? 2u
+                                      : (mine_covers_other && !other_covers_me) ? 0u : 1u;
+                const float half = axis == 0 ? ns.half_w : ns.half_h;
+                const float c = code == 0u || s == 0.0f ? 0.0f : (code == 2u ? 1.0f : 0.5f) * s * half * h2d;
+                const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
+                const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
+                const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float st = (float)(axis == 0 ? mA[k] : mB[k]) * (me_low ? 256.0f : -256.0f);
+                    const float g = c * ((2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2));
+                    acc[k * 3 + axis] += g;
+                    acc[k * 3 + 2] -= g * ndc;
+                }
+            }
+        } else {
         uint32_t codes = 0;
 #pragma unroll
         for (int dir = 0; dir < 4; ++dir) {
@@ -1496,6 +1533,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                 acc[k * 3 + axis] += g[k];
                 acc[k * 3 + 2] -= g[k] * ndc;
             }
+        }
         }
         // colour weights last: keeps their registers out of the pair loop's live range
         float lam[3];
