@@ -1245,6 +1245,11 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     {
         // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * 256)
         static_assert(kHaloPix <= 512, "two staging passes");
+        // frame base pointers (64-bit, uniform) + 32-bit per-lane offsets: H * W * C < 2^29
+        const int64_t fpix = (int64_t)b * H * W;
+        const int32_t *gb_f = gbuffer + fpix;
+        const uint8_t *cov_f = covbits + fpix;
+        const float *gp_f = grad_pixels + fpix * C, *px_f = pixels + fpix * C;
         int32_t gbv[2];
         uint32_t cvv[2];
         float Gv[2][CM], Iv[2][CM];
@@ -1257,14 +1262,14 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             gbv[u] = -2;
             cvv[u] = 0;
             if (ok[u]) {
-                const int64_t o = ((int64_t)b * H + (H - 1 - hj)) * W + hi;
-                gbv[u] = gbuffer[o];
-                cvv[u] = covbits[o];
+                const uint32_t o = (uint32_t)((H - 1 - hj) * W + hi);
+                gbv[u] = gb_f[o];
+                cvv[u] = cov_f[o];
 #pragma unroll
                 for (int c = 0; c < CM; ++c)
                     if (c < C) {
-                        Gv[u][c] = grad_pixels[o * C + c];
-                        Iv[u][c] = pixels[o * C + c];
+                        Gv[u][c] = gp_f[o * C + c];
+                        Iv[u][c] = px_f[o * C + c];
                     }
             }
         }
@@ -1360,8 +1365,13 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     // ---- phase B: per-pixel contributions to the face visible at this pixel
     const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
     if (in_frame) {
-        const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
-        for (int c = 0; c < C; ++c) grad_bg[o * C + c] = rp < 0 ? s_G[kme * CP + c] : 0.0f;
+        float *gbg_f = grad_bg + (int64_t)b * H * W * C;
+        const uint32_t o = (uint32_t)((H - 1 - j) * W + i);
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+            const float gv = s_G[kme * CP + c];
+            if (c < C) gbg_f[o * C + c] = rp < 0 ? gv : 0.0f;
+        }
     }
 
     float acc[NVM];
@@ -1436,14 +1446,14 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                 const int klo = me_low ? kme : kq;
                 const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
                 const int32_t rq = gq & kGbufIndexMask;
+                const uint32_t covq = s_cov[kq];  // read unconditionally: the code below is all selects
                 const bool mine_covers_other = (covme >> dir) & 1u;
-                const bool other_covers_me = (s_cov[kq] >> (dir ^ 1)) & 1u;
+                const bool other_covers_me = (covq >> (dir ^ 1)) & 1u;
                 // 2: whole, 1: half, 0: none; -2 = outside the frame, -1 = background
-                const uint32_t code = gq == -2 ? 0u
-                                      : gq < 0 ? 2u
-                                      : rq == rp ? (me_low ? 2u : 0u)
-                                      : (!mine_covers_other && other_covers_me) ? 2u
-                                      : (mine_covers_other && !other_covers_me) ? 0u : 1u;
+                uint32_t code = (!mine_covers_other && other_covers_me) ? 2u : (mine_covers_other && !other_covers_me) ? 0u : 1u;
+                code = rq == rp ? (me_low ? 2u : 0u) : code;
+                code = gq < 0 ? 2u : code;
+                code = gq == -2 ? 0u : code;
                 const float half = axis == 0 ? ns.half_w : ns.half_h;
                 const float c = code == 0u || s == 0.0f ? 0.0f : (code == 2u ? 1.0f : 0.5f) * s * half * h2d;
                 const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
