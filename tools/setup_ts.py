@@ -40,11 +40,11 @@ def main():
     print("setup_kernel<128>: " + " ".join("%.2f" % x for x in times) + " us")
     ts = np.zeros((nwg, 13), np.uint64)
     _lib.check(rd(ts.ctypes.data, nwg))
-    S = ts[:, [0, 10, 11, 12, 1]].astype(np.int64)
+    S = ts[:, [0, 10, 11, 1]].astype(np.int64)
     ok = (S > 0).all(1)
     dS = np.diff(S[ok], axis=1)
-    for k, name in enumerate(["start -> faces arrived", "faces -> vertices arrived", "vertices -> record computed",
-                              "record -> phase end (stores issued)"]):
+    for k, name in enumerate(["start -> faces arrived", "faces -> vertices arrived",
+                              "vertices -> records computed and stored"]):
         print("  thread 0: %-36s median %7.0f  p90 %7.0f ticks" % (name, np.median(dS[:, k]), np.percentile(dS[:, k], 90)))
     T = ts[:, [0, 1, 2, 3, 7]].astype(np.int64)
     d = np.diff(T, axis=1)
