@@ -1797,6 +1797,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
                                                       vertices, camera_pos, shader_id, tcb)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
+    else if (C == 7) LAUNCH_RASTER(7);
     else LAUNCH_RASTER(0);
 #undef LAUNCH_RASTER
 #undef LAUNCH_PROC
@@ -1871,6 +1872,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
                                                     grad_background, ndc_scale(W, H))
     if (C == 1) LAUNCH_GRAD(1);
     else if (C == 3) LAUNCH_GRAD(3);
+    else if (C == 7) LAUNCH_GRAD(7);
     else LAUNCH_GRAD(0);
 #undef LAUNCH_GRAD
     HIP_TRY(hipGetLastError());
