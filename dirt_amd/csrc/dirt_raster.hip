@@ -1467,6 +1467,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                     acc[k * 3 + 2] -= g * ndc;
                 }
             }
+            PHASE_TS(11 + (acc[0] == 12345.f));
         } else {
         uint32_t codes = 0;
 #pragma unroll
