@@ -650,6 +650,28 @@ __device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__re
 __device__ __noinline__ bool covers_face_multi(int64_t hint_ri, const Rec *frame_recs, const FaceData *fdata_frame,
                                                int F, int f, int i, int j);
 
+// correctly rounded int64 -> float of three values, out of line (rare: |E| >= 2^31)
+__device__ __noinline__ float3 i64x3_to_f32(int64_t a, int64_t b, int64_t c)
+{
+    return make_float3((float)a, (float)b, (float)c);
+}
+
+// neighbour_coverage() without the int32 shortcut: int64 edge values, out of line (rare)
+__device__ __noinline__ uint32_t neighbour_bits_i64(const EdgePart &r, int64_t E0, int64_t E1, int64_t E2)
+{
+    const int64_t E[3] = {E0, E1, E2};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int dir = 0; dir < 4; ++dir) {
+        const int axis = dir >> 1, sg = (dir & 1) ? -1 : 1;
+        int64_t Eq[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Eq[k] = E[k] + (int64_t)(axis == 0 ? r.A[k] : r.B[k]) * (256 * sg);
+        bits |= (inside(r, Eq) ? 1u : 0u) << dir;
+    }
+    return bits;
+}
+
 // Bit d of the result: the face visible at pixel (i, j) (record r, E = its edge values there) also
 // covers the neighbour in direction d (0 right, 1 left, 2 up, 3 down; window coordinates) -- exactly
 // the coverage tests of the backward's pairs, computed once here for every pixel, so the
@@ -659,33 +681,37 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
                                                        const Rec *frame_recs, const FaceData *fdata_frame, int F, int f,
                                                        int i, int j)
 {
-    // int32 when every lane's |E| < 2^30 and |A|, |B| < 2^22 (a one-pixel step stays inside int32)
+    // int32 when every lane's |E| < 2^30 and |A|, |B| < 2^22 (a one-pixel step stays inside int32);
+    // otherwise the out-of-line int64 version (a real branch, not both paths)
     bool small = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k)
-        small = small && E[k] > -(1ll << 30) && E[k] < (1ll << 30) && r.A[k] > -(1 << 22) && r.A[k] < (1 << 22) &&
-                r.B[k] > -(1 << 22) && r.B[k] < (1 << 22);
-    const bool all_small = __builtin_amdgcn_ballot_w64(!small) == 0;
-    int32_t eo[3];  // E + owned
-#pragma unroll
-    for (int k = 0; k < 3; ++k) eo[k] = (int32_t)E[k] + ((r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0)) ? 1 : 0);
+        small = small && (uint64_t)(E[k] + (1ll << 30)) < (2ull << 30) && (uint32_t)(r.A[k] + (1 << 22)) < (2u << 22) &&
+                (uint32_t)(r.B[k] + (1 << 22)) < (2u << 22);
     uint32_t bits = 0;
+    if (__builtin_amdgcn_ballot_w64(!small) == 0) {
+        int32_t eo[3];  // E + owned
 #pragma unroll
-    for (int dir = 0; dir < 4; ++dir) {
-        const int axis = dir >> 1, sg = (dir & 1) ? -1 : 1;
-        bool c;
-        if (all_small) {
-            c = true;
+        for (int k = 0; k < 3; ++k) eo[k] = (int32_t)E[k] + ((r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0)) ? 1 : 0);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) c = c && eo[k] + (axis == 0 ? r.A[k] : r.B[k]) * (256 * sg) > 0;
-        } else {
-            int64_t Eq[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) Eq[k] = E[k] + (int64_t)(axis == 0 ? r.A[k] : r.B[k]) * (256 * sg);
-            c = inside(r, Eq);
+        for (int dir = 0; dir < 4; ++dir) {
+            const int axis = dir >> 1, sg = (dir & 1) ? -256 : 256;
+            const int32_t q0 = eo[0] + (axis == 0 ? r.A[0] : r.B[0]) * sg;
+            const int32_t q1 = eo[1] + (axis == 0 ? r.A[1] : r.B[1]) * sg;
+            const int32_t q2 = eo[2] + (axis == 0 ? r.A[2] : r.B[2]) * sg;
+            bits |= (min(q0, min(q1, q2)) > 0 ? 1u : 0u) << dir;
         }
-        if (!c && multi) c = covers_face_multi(ri, frame_recs, fdata_frame, F, f, i + (axis == 0 ? sg : 0), j + (axis == 1 ? sg : 0));
-        bits |= (c ? 1u : 0u) << dir;
+    } else {
+        bits = neighbour_bits_i64(*reinterpret_cast<const EdgePart *>(&r), E[0], E[1], E[2]);
+    }
+    if (multi) {
+#pragma unroll
+        for (int dir = 0; dir < 4; ++dir) {
+            const int axis = dir >> 1, sg = (dir & 1) ? -1 : 1;
+            if (!((bits >> dir) & 1u) &&
+                covers_face_multi(ri, frame_recs, fdata_frame, F, f, i + (axis == 0 ? sg : 0), j + (axis == 1 ? sg : 0)))
+                bits |= 1u << dir;
+        }
     }
     return bits;
 }
@@ -912,12 +938,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
 #pragma unroll
     for (int k = 0; k < 3; ++k) fits = fits && E[k] == (int64_t)(int32_t)E[k];
     float fE[3];
-    if (__builtin_amdgcn_ballot_w64(!fits) == 0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) fE[k] = (float)(int32_t)E[k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) fE[k] = (float)E[k];
+    for (int k = 0; k < 3; ++k) fE[k] = (float)(int32_t)E[k];
+    if (__builtin_amdgcn_ballot_w64(!fits) != 0) {  // (a real branch: the int64 conversions are not inlined)
+        const float3 w = i64x3_to_f32(E[0], E[1], E[2]);
+        fE[0] = w.x; fE[1] = w.y; fE[2] = w.z;
     }
     parent_lambda_f(r, fE, fd.clipped == 0, lam);
     if constexpr (SH == DIRT_SHADER_OCEANIC_HORIZON) {
