@@ -100,9 +100,10 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
                   const float *camera_pos, int B, int H, int W, int C, int V, int F,
                   float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch,
                   size_t scratch_bytes, int64_t bin_capacity, void *stream);
-/* flags of dirt_rasterise_fwd.  Every forward returns the scratch's bin counters to zero when it
- * completes, so a scratch buffer that was zero-filled once (or passed to dirt_scratch_clear) and since
- * used only by forwards with the same B, H, W, F and bin_capacity is "clean". */
+/* flags of dirt_rasterise_fwd.  Every forward leaves the scratch ready for the next one (the bin counts
+ * alternate between two sets, each zeroed by the forward that does not use it), so a scratch buffer that
+ * was zero-filled once (or passed to dirt_scratch_clear) and since used only by forwards with the same
+ * B, H, W, F and bin_capacity is "clean". */
 #define DIRT_FWD_SCRATCH_CLEAN 1u /* the scratch is clean: skip the forward's own clearing memset */
 /* zero_grad_vertices [B,V,4] / zero_grad_vertex_colors [B,V,C] (each may be NULL): accumulators the
  * forward zero-fills in passing (inside its raster kernel), for a later dirt_rasterise_bwd with
@@ -126,7 +127,8 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
 int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *scratch, size_t scratch_bytes,
                        void *stream);
 
-/* Debug check (synchronises `stream`): returns DIRT_EFACE if any face index is outside [0,V). */
+/* Debug check (synchronises `stream`): returns DIRT_EFACE if any face index is outside [0,V).  Uses the
+ * first 4 bytes of `scratch` as its flag: pass a scratch that no forward is using, or clear it after. */
 int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, size_t scratch_bytes, void *stream);
 
 /* Optional per-kernel timing with HIP events around every launch (used by bench.py for the roofline).
