@@ -1088,7 +1088,7 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
 }
 
 #ifndef DIRT_GRAD_WAVES
-#define DIRT_GRAD_WAVES 4  // min waves per SIMD the register allocation must allow
+#define DIRT_GRAD_WAVES 6  // min waves per SIMD the register allocation must allow
 #endif
 #ifndef DIRT_GRAD_ATTR
 #define DIRT_GRAD_ATTR
@@ -1458,9 +1458,14 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
         PHASE_TS(10 + (fEp[0] == 12345.f));
         if (!(AB & 17) && __builtin_amdgcn_ballot_w64(multi) == 0) {
             // No clipped face in this wave: ownership and accumulation of the four pairs without
-            // branches (the four directions interleave).  A neighbour shows my face iff it shows my
-            // record (a non-clipped face has exactly one), so no face_of_record per pair.
+            // branches.  A neighbour shows my face iff it shows my record (a non-clipped face has exactly
+            // one).  Ownership code: outside the frame 0, background 2, same face 2 for the
+            // lower pixel of the pair / 0 for the upper, else 1 + (q's face covers p) - (p's face covers q).
+            // The pair weight of vertex k is c_d * m_k with m_k = (2 E_k +- 256 A_k (or B_k)) / w_k =
+            // P_k +- Q_k and c_d = code_d * s_d * (W/2 or H/2) / (4D), so the two pairs of an axis fold
+            // into (c_0 + c_1) P_k + (c_0 - c_1) Q_k (and the same with the NDC factors for w).
             const uint32_t covme = s_cov[kme];
+            float cd[4];
 #pragma unroll
             for (int dir = 0; dir < 4; ++dir) {
                 const int axis = dir >> 1;
@@ -1468,29 +1473,30 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
                 const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
                 const int kq = kme + dj * kHalo + di;
                 const int32_t gq = s_gb[kq];
-                const int klo = me_low ? kme : kq;
-                const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
-                const int32_t rq = gq & kGbufIndexMask;
                 const uint32_t covq = s_cov[kq];  // read unconditionally: the code below is all selects
-                const bool mine_covers_other = (covme >> dir) & 1u;
-                const bool other_covers_me = (covq >> (dir ^ 1)) & 1u;
-                // 2: whole, 1: half, 0: none; -2 = outside the frame, -1 = background
-                uint32_t code = (!mine_covers_other && other_covers_me) ? 2u : (mine_covers_other && !other_covers_me) ? 0u : 1u;
-                code = rq == rp ? (me_low ? 2u : 0u) : code;
-                code = gq < 0 ? 2u : code;
-                code = gq == -2 ? 0u : code;
-                const float half = axis == 0 ? ns.half_w : ns.half_h;
-                const float c = code == 0u || s == 0.0f ? 0.0f : (code == 2u ? 1.0f : 0.5f) * s * half * h2d;
-                const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
-                const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
-                const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
+                const float s = axis == 0 ? s_sx[me_low ? kme : kq] : s_sy[me_low ? kme : kq];
+                const int32_t rq = gq & kGbufIndexMask;
+                int code = 1 + (int)((covq >> (dir ^ 1)) & 1u) - (int)((covme >> dir) & 1u);
+                code = rq == rp ? (me_low ? 2 : 0) : code;
+                code = gq < 0 ? 2 : code;
+                code = gq == -2 ? 0 : code;
+                const float K = (axis == 0 ? ns.half_w : ns.half_h) * h2d * 0.5f;
+                cd[dir] = code == 0 ? 0.0f : ((float)code * s) * K;
+            }
+            const float ndc_r = (float)(i + 1) * inv_hw - 1.0f, ndc_l = (float)i * inv_hw - 1.0f;
+            const float ndc_u = (float)(j + 1) * inv_hh - 1.0f, ndc_d = (float)j * inv_hh - 1.0f;
+            const float ux = cd[0] + cd[1], vx = cd[0] - cd[1];
+            const float uwx = cd[0] * ndc_r + cd[1] * ndc_l, vwx = cd[0] * ndc_r - cd[1] * ndc_l;
+            const float uy = cd[2] + cd[3], vy = cd[2] - cd[3];
+            const float uwy = cd[2] * ndc_u + cd[3] * ndc_d, vwy = cd[2] * ndc_u - cd[3] * ndc_d;
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float st = (float)(axis == 0 ? mA[k] : mB[k]) * (me_low ? 256.0f : -256.0f);
-                    const float g = c * ((2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2));
-                    acc[k * 3 + axis] += g;
-                    acc[k * 3 + 2] -= g * ndc;
-                }
+            for (int k = 0; k < 3; ++k) {
+                const float iwk = k == 0 ? iw0 : k == 1 ? iw1 : iw2;
+                const float P = (2.0f * fEp[k]) * iwk;
+                const float Qx = ((float)mA[k] * 256.0f) * iwk, Qy = ((float)mB[k] * 256.0f) * iwk;
+                acc[k * 3 + 0] += ux * P + vx * Qx;
+                acc[k * 3 + 1] += uy * P + vy * Qy;
+                acc[k * 3 + 2] -= (uwx * P + vwx * Qx) + (uwy * P + vwy * Qy);
             }
             PHASE_TS(11 + (acc[0] == 12345.f));
         } else {
