@@ -211,6 +211,35 @@ def test_session_and_hip_graph_replay_match_autograd():
     assert_close_grad(sess.grad_vertices.cpu().numpy(), ref["grad_vertices"], "graph grad_vertices")
 
 
+def test_session_alternating_scenes_keep_bins_clean():
+    # the bin counts alternate between two sets by a device-held parity: consecutive
+    # forwards over different scenes, forwards without a backward, and an odd number of graph replays
+    # must all see clean counts
+    from dirt_amd.session import RasteriseSession
+    scenes_ = [tuple(a[None] for a in scenes.random_triangles(F=2500, W=160, H=128, radius_px=r, seed=sd))
+               for sd, r in ((21, 9.0), (22, 20.0))]
+    refs = [run_gpu(*sc) for sc in scenes_]
+    dev = torch.device("cuda", 0)
+    sess = RasteriseSession(1, 128, 160, 3, 7500, 2500, device=dev)
+    tss = [[torch.from_numpy(a).to(dev) for a in sc] for sc in scenes_]
+    for k in (0, 1, 1, 0, 1, 0, 0):
+        sess.forward(*tss[k])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sess.pixels.cpu().numpy(), refs[k]["pixels"])
+        np.testing.assert_array_equal(sess.gbuffer.cpu().numpy(), refs[k]["gbuffer"])
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        sess.forward(*tss[1])
+    for _ in range(3):
+        sess.pixels.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sess.pixels.cpu().numpy(), refs[1]["pixels"])
+    sess.forward(*tss[0])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(sess.pixels.cpu().numpy(), refs[0]["pixels"])
+
+
 def _gpu_shard_worker(rank, world, port, inputs, outq):
     import torch.distributed as dist
     from dirt_amd.sharding import rasterise_batch_sharded
