@@ -10,8 +10,8 @@
 //   K3 fill_kernel     every workgroup scans its frame's per-tile totals into bin offsets (frame-local
 //                      bin regions), then scatters each record index into the coarse bins it overlaps.
 //                      (K2, a separate scan launch, no longer exists; its profile slot stays empty.)
-//   K4 raster_kernel   one 256-thread workgroup per 16x16 tile (a wave per 16x4 strip): stages the
-//                      tile's records in LDS with strip-relative 32-bit edge values (exact), each lane
+//   K4 raster_kernel   one 256-thread workgroup per 16x16 tile (a wave per 8x8 block): stages the
+//                      tile's records in LDS with tile-relative 32-bit edge values (exact), each lane
 //                      owns one pixel and keeps the min (depth24<<32 | face) key, then resolves
 //                      in-kernel: perspective-correct Gouraud colour (R6) or background, coalesced
 //                      [B,H,W,C] writes + the int32 g-buffer.  This fuses the reference's
@@ -495,6 +495,15 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
 // Results are bit-identical to R3/R4 (oracle) by construction.
 
 constexpr int kStrips = 4;
+// The pixels a wave owns inside its 16x16 tile: an 8x8 block (DIRT_RASTER_STRIPS=0, default) or a 16x4
+// strip.  A block is the more compact shape: fewer triangles overlap it (Steiner: the overlap area of a
+// region and a triangle grows with the region's perimeter, 32 vs 40 px), so fewer entries per wave.
+#ifndef DIRT_RASTER_STRIPS
+#define DIRT_RASTER_STRIPS 0
+#endif
+constexpr int kWaveW = DIRT_RASTER_STRIPS ? 16 : 8, kWaveH = DIRT_RASTER_STRIPS ? 4 : 8;
+__host__ __device__ constexpr int wave_ox(int w) { return DIRT_RASTER_STRIPS ? 0 : 8 * (w & 1); }
+__host__ __device__ constexpr int wave_oy(int w) { return DIRT_RASTER_STRIPS ? 4 * w : 8 * (w >> 1); }
 // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 shares an L2),
 // so give each residue class a contiguous band of tiles; neighbouring tiles then share halo pixels and
 // records in one L2.  A bijection on [0, n); speed only, never correctness.
@@ -566,8 +575,8 @@ __device__ __forceinline__ void wave_lds_sync()
 
 // Stage one tile survivor (record ri) for the 16x16 tile at pixel (ti0, tj0): edge values at the tile
 // origin (E + owned, exact int32, pinned to 2^30 where the edge holds over the whole tile), the packed
-// (A, B) steps, depth plane and key.  Returns the mask of the tile's four 16x4 strips the record can
-// cover (its rows overlap the strip and no edge excludes the whole strip; exact int64 tests) and sets
+// (A, B) steps, depth plane and key.  Returns the mask of the tile's four wave rectangles (8x8 blocks) the
+// record can cover (its bbox overlaps the block and no edge excludes the whole block; exact int64 tests) and sets
 // `large` when the record needs the per-lane int64 path (some |A|, |B| >= 2^15).
 __device__ __forceinline__ uint32_t stage_tile(const Rec *__restrict__ frame_recs, int32_t ri, int ti0, int tj0, int F,
                                                StripEntry &E, bool &large)
@@ -580,21 +589,25 @@ __device__ __forceinline__ uint32_t stage_tile(const Rec *__restrict__ frame_rec
     uint32_t mask = 0;
 #pragma unroll
     for (int st = 0; st < kStrips; ++st) {
-        const int sj0 = tj0 + 4 * st;
-        if ((int)R.j0 <= sj0 + 3 && (int)R.j1 >= sj0) mask |= 1u << st;
+        const int x0 = ti0 + wave_ox(st), y0 = tj0 + wave_oy(st);
+        if ((int)R.i0 <= x0 + kWaveW - 1 && (int)R.i1 >= x0 && (int)R.j0 <= y0 + kWaveH - 1 && (int)R.j1 >= y0)
+            mask |= 1u << st;
     }
     const int32_t px0 = ti0 * 256 + 128, py0 = tj0 * 256 + 128;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
         const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
-        const int64_t sx = (int64_t)R.A[k] * (15 * 256), by = (int64_t)R.B[k] * (4 * 256);
-        const int64_t xmax = sx > 0 ? sx : 0, xmin = sx < 0 ? sx : 0;
-        const int64_t ymax3 = by > 0 ? 3 * (by >> 2) : 0, ymin15 = by < 0 ? 15 * (by >> 2) : 0;
+        const int64_t a = (int64_t)R.A[k] * 256, bb = (int64_t)R.B[k] * 256;
+        // over a wave's rectangle [ox, ox + kWaveW) x [oy, oy + kWaveH): max of E at its origin + the
+        // positive parts of the steps across it
+        const int64_t wx = a * (kWaveW - 1), wy = bb * (kWaveH - 1);
+        const int64_t wmax = (wx > 0 ? wx : 0) + (wy > 0 ? wy : 0);
 #pragma unroll
         for (int st = 0; st < kStrips; ++st)
-            if (e0 + xmax + st * by + ymax3 <= 0) mask &= ~(1u << st);
-        E.e[k] = e0 + xmin + ymin15 > 0 ? (1 << 30) : (int32_t)e0;
+            if (e0 + a * wave_ox(st) + bb * wave_oy(st) + wmax <= 0) mask &= ~(1u << st);
+        const int64_t tx = a * (kTile - 1), ty = bb * (kTile - 1);
+        E.e[k] = e0 + (tx < 0 ? tx : 0) + (ty < 0 ? ty : 0) > 0 ? (1 << 30) : (int32_t)e0;
         E.ab[k] = ((uint32_t)R.A[k] & 0xffffu) | ((uint32_t)R.B[k] << 16);
     }
     if (!small) {
@@ -762,8 +775,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     // interleaved over the XCDs instead (round-robin dispatch order) for balance
     const int tile = SH == DIRT_SHADER_GOURAUD ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x, b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
-    const int t = threadIdx.x, lx = t & 15, ly = t >> 4, lane = t & 63;
+    const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int lx = wave_ox(wave) + lane % kWaveW, ly = wave_oy(wave) + lane / kWaveW;
     const int i = tx * kTile + lx, j = ty * kTile + ly;
     const int dx = lx * 256, dy = ly * 256;  // offset from the tile origin (sub-pixels)
     const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
