@@ -482,16 +482,16 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
 // ------------------------------------------------------------------------------------------------
 // K4: tile raster + resolve
 //
-// One workgroup per 16x16 tile; each of its 4 waves owns a 16x4 strip and works independently of
-// the others (wave-private LDS, no workgroup barriers):
-//   a. filter the coarse bin by the packed bbox against the strip, compacting survivors (ballot);
-//   b. per survivor (one lane each) evaluate the int64 edge functions at the strip origin, fold in
-//      the top-left bias (E + owned > 0 <=> inside) and classify each edge over the strip:
-//      all-outside -> dropped, all-inside -> pinned to 2^30, straddling -> exact int32 value;
-//      survivors are compacted again into a 64-B LDS entry;
-//   c. every lane (pixel) steps the three edges with 24-bit multiply-adds -- exact for triangles
-//      with |A|,|B| < 2^16 (|E| < 2^29 over a strip); larger ones use per-lane int64 (flagged) --
-//      and keeps the min (depth24<<32 | face) key.
+// One workgroup per 16x16 tile; each of its 4 waves owns an 8x8 block of it:
+//   a. the workgroup filters its coarse slab once (a quarter of every 512-entry chunk per wave) by the
+//      packed bbox against the tile, compacting survivors into per-wave LDS segments (ballot);
+//   b. the survivors are staged once, an entry per thread: int64 edge functions at the tile origin with
+//      the top-left bias folded in (E + owned > 0 <=> inside), pinned to 2^30 where an edge holds over
+//      the whole tile, else exact int32; packed i16 (A, B); the depth plane; the exact mask of the
+//      blocks the record can cover;
+//   c. each wave walks the entries of its block: three v_dot2_i32_i16 edge steps (exact for records with
+//      |A|, |B| < 2^15; larger ones use per-lane int64, flagged), two FMAs of depth and a branch-free
+//      min of the 64-bit (depth24 << 32 | face << 3 | s) key.
 // Results are bit-identical to R3/R4 (oracle) by construction.
 
 constexpr int kStrips = 4;
