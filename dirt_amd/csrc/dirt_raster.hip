@@ -749,21 +749,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      int sid, int tcb)
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
-    if (!(AB & 16)) {
-        // housekeeping spread over all blocks (a few KB each): zero-fill the caller's gradient
-        // accumulators if it passed them (the bin counts are returned to zero by their last reader)
-        const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
-        const int64_t gt = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x, gs = nblk * 256;
-        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (zero_a) {
-            for (int64_t k = gt; k < (nzero_a >> 2); k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
-            for (int64_t k = (nzero_a & ~3LL) + gt; k < nzero_a; k += gs) zero_a[k] = 0.f;
-        }
-        if (zero_b) {
-            for (int64_t k = gt; k < (nzero_b >> 2); k += gs) reinterpret_cast<float4 *>(zero_b)[k] = z4;
-            for (int64_t k = (nzero_b & ~3LL) + gt; k < nzero_b; k += gs) zero_b[k] = 0.f;
-        }
-    }
+    PHASE_TS(0);
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     const int C = CC > 0 ? CC : Cdyn;
     __shared__ int32_t t_list[kStrips][kFilterBlock];  // per-wave segments of the tile's survivors
@@ -793,13 +779,42 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const int cx = ti0 >> cshift, cy = tj0 >> cshift;
     const int c = cy * nctx + cx;
     const int64_t cc = (int64_t)b * ncoarse + c;
-    const uint32_t par = flag[kParP] & 1u;
-    const uint32_t raw = F > 0 ? counts[par * (int64_t)B * ncoarse + cc] : 0u;  // F == 0: setup did not run
-    if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = par ^ 1u;
+    // The parity word, both count sets and the first chunk of the slab are loaded together (one memory
+    // round trip instead of three dependent ones): slab entries are loaded before the count is known,
+    // unconditionally (index clamped to the slab), and those past the count are masked afterwards.
+    const uint2 *slab_bins = bins + cc * slab;
+    constexpr int U = kFilterBlock / 64;
+    uint2 ev[U];
+    auto load_chunk = [&](uint32_t chunk) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = chunk + wave * kFilterBlock + u * 64 + lane;
+            ev[u] = slab_bins[min(idx, slab - 1u)];
+        }
+    };
+    if (slab > 0 && !(AB & 8)) load_chunk(0);
+    // This forward's setup zeroed the other count set, so the count is the sum of both (no dependent
+    // parity load); F == 0: setup did not run
+    const uint32_t raw = F > 0 ? counts[cc] + counts[(int64_t)B * ncoarse + cc] : 0u;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
+    if (!(AB & 16)) {
+        // housekeeping spread over all blocks (a few KB each): zero-fill the caller's gradient
+        // accumulators if it passed them (after the slab loads are in flight)
+        const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
+        const int64_t gt = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x, gs = nblk * 256;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (zero_a) {
+            for (int64_t k = gt; k < (nzero_a >> 2); k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
+            for (int64_t k = (nzero_a & ~3LL) + gt; k < nzero_a; k += gs) zero_a[k] = 0.f;
+        }
+        if (zero_b) {
+            for (int64_t k = gt; k < (nzero_b >> 2); k += gs) reinterpret_cast<float4 *>(zero_b)[k] = z4;
+            for (int64_t k = (nzero_b & ~3LL) + gt; k < nzero_b; k += gs) zero_b[k] = 0.f;
+        }
+    }
     // an overflowed slab (more pairs than its capacity): filter every record of the frame instead
     const bool overflow = raw > slab;
     const uint32_t n_items = overflow ? (uint32_t)nrec : raw;
-    const uint2 *slab_bins = bins + cc * slab;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
     // tile rectangle relative to the coarse tile
     const uint32_t rx0 = (uint32_t)(ti0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
@@ -813,8 +828,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         // thread, with the mask of strips it can cover) and every wave rasterises the entries that reach
         // its strip.  Chunks and rounds are workgroup-uniform, so every thread meets every barrier.
         int par = 0;
-        for (uint32_t chunk = 0; chunk < n_items; chunk += kStrips * kFilterBlock, par ^= 1) {
-            constexpr int U = kFilterBlock / 64;
+        for (uint32_t chunk = 0; chunk == 0 || chunk < n_items; chunk += kStrips * kFilterBlock, par ^= 1) {
             uint32_t rid[U];
             bool keep_u[U];
 #pragma unroll
@@ -822,9 +836,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                 const uint32_t idx = chunk + wave * kFilterBlock + u * 64 + lane;
                 const bool ok = idx < n_items;
                 if (!overflow) {
-                    const uint2 ev = ok ? slab_bins[idx] : make_uint2(0u, 0u);
-                    const uint32_t bb = ev.y;
-                    rid[u] = ev.x;
+                    const uint32_t bb = ev[u].y;
+                    rid[u] = ev[u].x;
                     keep_u[u] = ok && (bb & 0xff) <= rx1 && ((bb >> 8) & 0xff) >= rx0 && ((bb >> 16) & 0xff) <= ry1 &&
                                 (bb >> 24) >= ry0;
                 } else {
@@ -854,6 +867,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             }
             if (lane == 0) t_nw[par][wave] = n_w;
             __syncthreads();
+            if (chunk == 0) PHASE_TS(1);
             int pre[kStrips + 1];
             pre[0] = 0;
 #pragma unroll
@@ -862,9 +876,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             if (AB & 2) {
                 best += (uint64_t)n_list;
                 __syncthreads();
-                continue;
             }
-            for (int from = 0; from < n_list; from += 256) {
+            for (int from = 0; from < ((AB & 2) ? 0 : n_list); from += 256) {
                 const int g = from + t;
                 uint32_t m = 0;
                 if (g < n_list) {
@@ -883,6 +896,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                 }
                 t_mask[t] = (uint8_t)m;
                 __syncthreads();
+                if (chunk == 0 && from == 0) PHASE_TS(2);
                 const int nst = min(256, n_list - from);
                 if (!(AB & 1)) {
                     for (int c0 = 0; c0 < nst; c0 += 64) {
@@ -923,8 +937,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                 // them only after its own filter barrier, and the last round needs no barrier at all
                 if (from + 256 < n_list) __syncthreads();
             }
+            // next chunk's slab entries (its filter runs after the next barrier-free LDS writes; t_list
+            // is rewritten only after this chunk's last staging round)
+            if (!overflow && chunk + kStrips * kFilterBlock < n_items) load_chunk(chunk + kStrips * kFilterBlock);
         }
     }
+    PHASE_TS(3);
     if (!in_frame) return;
     float *out = pixels + o * C;
     if (AB & 15) {
@@ -938,6 +956,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
 #pragma unroll
         for (int c2 = 0; c2 < CM; ++c2)
             if (c2 < C) out[c2] = kNoDepth ? 0.0f : background[o * C + c2];  // (hill: no background copy)
+        PHASE_TS(4);
+        PHASE_TS(5);
         return;
     }
     const Rec &r = frame_recs[best_rec];
@@ -959,6 +979,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         fE[0] = w.x; fE[1] = w.y; fE[2] = w.z;
     }
     parent_lambda_f(r, fE, fd.clipped == 0, lam);
+    PHASE_TS(4);
     if constexpr (SH == DIRT_SHADER_OCEANIC_HORIZON) {
         // texCoordV = perspective-correct clip xy (shaders.cpp:19,21 alias texCoord to position); jitter by
         // the background texel at (texCoordV+1)/2 (NEAREST), channels x,y (C=1 broadcast)
@@ -1015,6 +1036,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
         covbits[o] = (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, best_rec, frame_recs, fdata + (int64_t)b * F,
                                                  F, face_of_record(best_rec, F), i, j);
+        PHASE_TS(5);
     }
 }
 
@@ -1964,7 +1986,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
                                                              nullptr, 0, nullptr, nullptr, 0, C);                    \
         break
     switch (variant) {
-        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8);
+        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8); V_RAST(128);
     default:
         return fail(DIRT_EINVAL, "dirt_debug_raster_variant: unknown variant");
     }
