@@ -119,8 +119,8 @@ constexpr int64_t kDefaultBinBudget = 1ll << 27;  // entries (1 GiB) above which
 // Count-set parity, so that no kernel has to return the counts it read to zero.  Words of the flag area
 // (separate 64-B lines): [0] out-of-range-face flag, [kParP] P, [kParQ] Q.  The setup kernel reads p = Q,
 // publishes P = p, accumulates into counts[p] and zeroes counts[p ^ 1] (read by the previous forward's
-// raster, which has completed); the raster kernel reads p = P, bins from counts[p] and publishes
-// Q = p ^ 1 for the next forward.  Each word is only read by one kernel and only written (one workgroup,
+// raster, which has completed); the raster kernel bins from counts[0] + counts[1] (= counts[p], the
+// other set being zero) and publishes Q = P ^ 1 for the next forward.  Each word is only read by one kernel and only written (one workgroup,
 // one value) by the other, so no launch reads a word it writes.  Zeroed scratch = a valid state.
 constexpr int kParP = 16, kParQ = 32;
 
