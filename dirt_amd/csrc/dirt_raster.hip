@@ -730,7 +730,8 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
 }
 
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
-// staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too
+// staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too,
+// 32 no neighbour-coverage bits, 64 no colour loads (lambda written), 128 phase timestamps
 #ifndef DIRT_RASTER_WAVES
 #define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
                              // the procedural programs and the generic-C path keep their natural allocation)
@@ -1031,11 +1032,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                (float)W, (float)H);
         for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 2 ? col.z : k == 3 ? 1.0f : 0.0f;
     } else {
-        const float *cb = colors + (int64_t)b * V * C;
-        const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
-        for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
-        covbits[o] = (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, best_rec, frame_recs, fdata + (int64_t)b * F,
-                                                 F, face_of_record(best_rec, F), i, j);
+        if (AB & 64) {
+            for (int k = 0; k < C; ++k) out[k] = lam[k % 3];
+        } else {
+            const float *cb = colors + (int64_t)b * V * C;
+            const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
+            for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
+        }
+        covbits[o] = (AB & 32) ? (uint8_t)0
+                               : (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, best_rec, frame_recs,
+                                                             fdata + (int64_t)b * F, F, face_of_record(best_rec, F), i, j);
         PHASE_TS(5);
     }
 }
@@ -1986,7 +1992,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
                                                              nullptr, 0, nullptr, nullptr, 0, C);                    \
         break
     switch (variant) {
-        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8); V_RAST(128);
+        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8); V_RAST(32); V_RAST(64); V_RAST(96); V_RAST(128);
     default:
         return fail(DIRT_EINVAL, "dirt_debug_raster_variant: unknown variant");
     }

@@ -47,7 +47,8 @@ def main():
     rfn.argtypes = [ctypes.c_int, P, P, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, P, ctypes.POINTER(ctypes.c_float)]
     rfn.restype = ctypes.c_int
     RN = {0: "full", 1: "no pixel loop, no resolve", 2: "bin filter only, no resolve", 4: "no resolve",
-          8: "nothing (housekeeping + bg prefetch + gbuffer write)"}
+          8: "nothing (housekeeping + bg prefetch + gbuffer write)", 32: "no coverage bits",
+          64: "no colour loads", 96: "no coverage bits, no colour loads"}
     rres = {k: [] for k in RN}
     for rnd in range(30):
         for k in RN:
