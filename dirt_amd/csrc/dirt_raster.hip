@@ -1055,7 +1055,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
 // on the other side, same-face pairs by the lower lane only).  Reduction without global contention:
 //   1. DPP segmented scan along each 16-pixel row (one DPP row == one pixel row) sums runs of equal
 //      record index into the run's last lane;
-//   2. run tails ds_add into a per-tile LDS hash table keyed by record index (vertex ids cached);
+//   2. run tails write their partial sums into their record's contiguous LDS range (records kept in a
+//      per-tile LDS hash table keyed by record index, vertex ids cached);
 //   3. one wave-instruction of global float atomics per (tile, record): <= 9+3C lanes, ~3 cache lines.
 
 // Does face f cover pixel (i,j)?  `hint` is the record of f covering a neighbouring pixel; the other
@@ -1254,7 +1255,8 @@ __device__ __forceinline__ int run_start(int key, int lx)
 
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip pairs, 2 skip colour weights,
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
-// 32 skip the DPP run scan (every lane adds into LDS)
+// 32 skip the DPP run scan (every lane adds into LDS), 128 phase timestamps, 256 flush sums without
+// the global atomics
 template <int CC, int AB = 0>
 __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
@@ -1283,9 +1285,10 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     float *const s_I = s_u + kHaloPix * CP;
     float *const s_part = s_u;
     __shared__ SlotTable T;
-    __shared__ int32_t s_head[kSlots];   // per slot: linked list of its run tails
-    __shared__ int32_t s_next[kTailCap];
-    __shared__ int32_t s_ntail;
+    // per slot: its number of row runs (= run tails), then the start (a cursor during the tail phase)
+    // of its contiguous range of tail partials in s_part
+    __shared__ int32_t s_tcnt[kSlots];
+    __shared__ int32_t s_toff[kSlots];
 
     const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
@@ -1302,12 +1305,9 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     PHASE_TS(0);
     for (int k = t; k < kSlots; k += 256) {
         T.key[k] = -1;
-        s_head[k] = -1;
+        s_tcnt[k] = 0;
     }
-    if (t == 0) {
-        T.n = 0;
-        s_ntail = 0;
-    }
+    if (t == 0) T.n = 0;
     const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
     {
         // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * 256)
@@ -1372,6 +1372,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
         const int key = g >= 0 ? g : -1;
         const int start = run_start(key, lx);
         int slot = slot_insert_wave(T, key, key >= 0 && start == lx);
+        if (key >= 0 && start == lx && slot >= 0) atomicAdd(&s_tcnt[slot], 1);  // one run (one tail later)
         slot = __shfl(slot, (t & 48) + start, 64);
         s_slot[kme] = key >= 0 ? slot : -1;
     }
@@ -1379,7 +1380,19 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     PHASE_TS(2);
     PHASE_TS(3);
     const int nslots = T.n;
-    static_assert(kSlots <= 256, "one slot per thread");
+    static_assert(kSlots <= 64, "one slot per lane of wave 0");
+    if (t < 64) {
+        // wave 0: each slot's range of run-tail partials, in slot-list order (exclusive prefix)
+        const int sl = t < nslots ? T.list[t] : 0;
+        const int cnt = t < nslots ? s_tcnt[sl] : 0;
+        int inc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(inc, d, 64);
+            inc += t >= d ? v : 0;
+        }
+        if (t < nslots) s_toff[sl] = inc - cnt;
+    }
     {
         // slot fill: the record loads are issued first and land while the pair scalars are computed
         const bool filler = t < nslots;
@@ -1639,9 +1652,9 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     }
 
     // ---- phase C: segmented sum over runs of equal key along each 16-lane row (one DPP row); the
-    // run tails store their partial sums with plain LDS writes and push themselves onto their slot's
-    // list with one exchange (LDS float atomics serialise on shared addresses); tails without a
-    // slot (table full) add straight to global memory
+    // run tails store their partial sums with plain LDS writes into their slot's contiguous range
+    // (sized in phase A by counting run heads; LDS float atomics serialise on shared addresses); tails
+    // without a slot (table full) or past the partial buffer add straight to global memory
     const int key = rp >= 0 ? rp : -1;
     const int start = run_start(key, lx);
     // 0/1 multipliers: x += shifted(x) * m is one v_fmac with a DPP operand (exact: m is 0 or 1,
@@ -1668,23 +1681,15 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     __syncthreads();  // every read of s_G / s_I is done: the union now holds tail partials
     PHASE_TS(5);
     int q = -1;
-    {
-        const bool want = tail && sp >= 0;
-        const uint64_t mask = __ballot(want);
-        int base = 0;
-        if ((t & 63) == 0 && mask) base = atomicAdd(&s_ntail, __popcll(mask));
-        base = __shfl(base, 0, 64);
-        if (want) {
-            q = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            if (q >= kTailCap) q = -1;
-        }
+    if (tail && sp >= 0) {
+        q = atomicAdd(&s_toff[sp], 1);  // the next place in the slot's range
+        if (q >= kTailCap) q = -1;
     }
     if (tail) {
         if (q >= 0) {
 #pragma unroll
             for (int v = 0; v < NVM; ++v)
                 if (v < NV) s_part[q * NVM + v] = acc[v];
-            s_next[q] = atomicExch(&s_head[sp], q);
         } else {
             const FaceData &fd = fdata_frame[face_of_record(rp, F)];
             const int32_t vid[3] = {fd.v[0], fd.v[1], fd.v[2]};  // before the atomics (may alias for the compiler)
@@ -1700,7 +1705,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     PHASE_TS(6);
 
     // ---- phase D: flush.  Thread t handles component t % NV of slot t / NV, so every lane of the
-    // workgroup walks one short list in parallel; a slot's components go out as one run of lanes
+    // workgroup sums one slot's tails in parallel; a slot's components go out as one run of lanes
     // (~3 cache lines of global float atomics per (tile, record)).
     const int n = (AB & 8) ? 0 : nslots;
     const int per_round = 256 / NV;
@@ -1710,9 +1715,24 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
         const int slot = T.list[e];
         const int kv = comp_id < 9 ? comp_id / 3 : (comp_id - 9) / C;
         const int vid = T.v[kv][slot];
+        // the slot's tails are contiguous (the cursor now points past them): four reads in flight per step
+        const int end = s_toff[slot], beg = max(end - s_tcnt[slot], 0), hi = min(end, kTailCap);
         float val = 0.0f;
-        for (int q = s_head[slot]; q >= 0; q = s_next[q]) val += s_part[q * NVM + comp_id];
+        for (int q0 = beg; q0 < hi; q0 += 4) {
+            float a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int qq = q0 + u;
+                const float x = s_part[min(qq, hi - 1) * NVM + comp_id];
+                a[u] = qq < hi ? x : 0.0f;
+            }
+            val += (a[0] + a[1]) + (a[2] + a[3]);
+        }
         if (val == 0.0f) continue;
+        if (AB & 256) {  // ablation: sums without the global atomics
+            if (val == 12345.f) grad_verts[0] = val;
+            continue;
+        }
         if (comp_id < 9) {
             const int c3 = comp_id % 3;
             atomicAdd(gvb + (int64_t)vid * 4 + (c3 == 2 ? 3 : c3), val);
@@ -2070,7 +2090,7 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
         break
     switch (variant) {
         V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);
-        V_GRAD(32); V_GRAD(64); V_GRAD(72); V_GRAD(128);
+        V_GRAD(32); V_GRAD(64); V_GRAD(72); V_GRAD(128); V_GRAD(256);
     default:
         return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: unknown variant");
     }
