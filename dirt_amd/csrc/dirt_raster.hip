@@ -1156,7 +1156,7 @@ struct SlotTable {
     int32_t A[3][kSlots], B[3][kSlots];
     int32_t e[3][kSlots];      // small records: E + owned at the halo origin pixel (see kGradSmallEdge)
     uint32_t bx[kSlots], by[kSlots];  // i0 | i1 << 16 (bit 31: large record, use the global Rec)
-    int32_t v[3][kSlots];
+    int32_t v[3][kSlots];    // vertex ids, indexed by list position
     float iw[3][kSlots], w[3][kSlots];  // interpolation data of the record (own-pixel path)
     float h2d[kSlots];                  // 1 / (2 D), D = E0 + E1 + E2 (constant over the plane)
     int32_t n;
@@ -1289,6 +1289,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     // of its contiguous range of tail partials in s_part
     __shared__ int32_t s_tcnt[kSlots];
     __shared__ int32_t s_toff[kSlots];
+    __shared__ int32_t s_lbeg[kSlots], s_lcnt[kSlots];  // the same ranges by list position (flush)
 
     const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
     const int tx = tile % ntx, ty = tile / ntx;
@@ -1391,7 +1392,11 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
             const int v = __shfl_up(inc, d, 64);
             inc += t >= d ? v : 0;
         }
-        if (t < nslots) s_toff[sl] = inc - cnt;
+        if (t < nslots) {
+            s_toff[sl] = inc - cnt;
+            s_lbeg[t] = inc - cnt;
+            s_lcnt[t] = cnt;
+        }
     }
     {
         // slot fill: the record loads are issued first and land while the pair scalars are computed
@@ -1427,7 +1432,7 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 T.A[k][sf] = ep.A[k]; T.B[k][sf] = ep.B[k];
-                T.v[k][sf] = fd.v[k];
+                T.v[k][t] = fd.v[k];  // by list position (read only by the flush)
                 T.w[k][sf] = fd.w[k];
                 small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
                         ep.B[k] < kGradSmallEdge;
@@ -1712,11 +1717,10 @@ __global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kern
     for (int e0 = 0; e0 < n; e0 += per_round) {
         const int e = e0 + t / NV, comp_id = t - (t / NV) * NV;
         if (t >= per_round * NV || e >= n) continue;
-        const int slot = T.list[e];
         const int kv = comp_id < 9 ? comp_id / 3 : (comp_id - 9) / C;
-        const int vid = T.v[kv][slot];
-        // the slot's tails are contiguous (the cursor now points past them): four reads in flight per step
-        const int end = s_toff[slot], beg = max(end - s_tcnt[slot], 0), hi = min(end, kTailCap);
+        const int vid = T.v[kv][e];
+        // the record's tails are contiguous: four reads in flight per step
+        const int beg = s_lbeg[e], hi = min(beg + s_lcnt[e], kTailCap);
         float val = 0.0f;
         for (int q0 = beg; q0 < hi; q0 += 4) {
             float a[4];
