@@ -450,7 +450,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     uint32_t *cc = ccount + (int64_t)b * ncoarse;
     for (int c = t; c < ncoarse; c += kBinThreads) {
         const uint32_t n = hist[c];
-        base[c] = n ? atomicAdd(&cc[c], n) : 0u;
+        base[c] = (AB & 1) ? 0u : n ? atomicAdd(&cc[c], n) : 0u;  // (AB & 1: ablation, no reservation)
         hist[c] = 0;
     }
     __syncthreads();
@@ -2032,8 +2032,9 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
 
 // Instrumented setup (tools/setup_ts.py): clean scratch, one setup_kernel<128> launch, its time in ms;
 // per-workgroup phase timestamps land in g_phase_ts (dirt_debug_read_phase_ts).
-int dirt_debug_setup_ts(const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F, void *saved,
-                        void *scratch, void *stream_, float *ms)
+// variant 0: timestamps, 1: timestamps without the slab reservation atomics, 2 / 3: the same untimestamped
+int dirt_debug_setup_ts(int variant, const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F,
+                        void *saved, void *scratch, void *stream_, float *ms)
 {
     Layout L;
     int rc = make_layout(B, H, W, F, 0, L);
@@ -2051,9 +2052,18 @@ int dirt_debug_setup_ts(const float *vertices, const int32_t *faces, int B, int 
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, stream));
-    setup_kernel<128><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
-                                                                   L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
-                                                                   L.slab, B);
+    switch (variant) {
+#define V_SETUP(K, AB)                                                                                        \
+    case K:                                                                                                   \
+        setup_kernel<AB><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift,      \
+                                                                     L.nctx, L.ncoarse, L.nrec, recs, fdata,     \
+                                                                     ccount, flag, bins, L.slab, B);            \
+        break
+        V_SETUP(0, 128); V_SETUP(1, 129); V_SETUP(2, 0); V_SETUP(3, 1);
+#undef V_SETUP
+    default:
+        return fail(DIRT_EINVAL, "dirt_debug_setup_ts: unknown variant");
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, stream));
     HIP_TRY(hipEventSynchronize(e1));

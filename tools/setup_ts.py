@@ -26,15 +26,22 @@ def main():
     lib = _lib.load()
     fn = lib.dirt_debug_setup_ts
     P = ctypes.c_void_p
-    fn.argtypes = [P, P] + [ctypes.c_int] * 5 + [P, P, P, ctypes.POINTER(ctypes.c_float)]
+    fn.argtypes = [ctypes.c_int, P, P] + [ctypes.c_int] * 5 + [P, P, P, ctypes.POINTER(ctypes.c_float)]
     rd = lib.dirt_debug_read_phase_ts
     rd.argtypes = [P, ctypes.c_int]
     stream = torch.cuda.current_stream().cuda_stream
     ms = ctypes.c_float(0)
     nwg = (F + 255) // 256 * B
+    for variant, name in ((2, "plain"), (3, "plain, no reservation atomics"), (1, "timestamps, no reservation")):
+        tv = []
+        for _ in range(20):
+            _lib.check(fn(variant, t[1].data_ptr(), t[3].data_ptr(), B, H, W, V, F, sess.saved.data_ptr(),
+                          sess.scratch.data_ptr(), stream, ctypes.byref(ms)))
+            tv.append(ms.value * 1e3)
+        print("setup variant %-32s median %.2f us" % (name, float(np.median(tv))))
     times = []
     for _ in range(5):
-        _lib.check(fn(t[1].data_ptr(), t[3].data_ptr(), B, H, W, V, F, sess.saved.data_ptr(), sess.scratch.data_ptr(),
+        _lib.check(fn(0, t[1].data_ptr(), t[3].data_ptr(), B, H, W, V, F, sess.saved.data_ptr(), sess.scratch.data_ptr(),
                       stream, ctypes.byref(ms)))
         times.append(ms.value * 1e3)
     print("setup_kernel<128>: " + " ".join("%.2f" % x for x in times) + " us")
