@@ -1133,6 +1133,10 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
 #ifndef DIRT_GRAD_WAVES
 #define DIRT_GRAD_WAVES 6  // min waves per SIMD the register allocation must allow
 #endif
+#ifndef DIRT_GRAD_WAVES_C3
+#define DIRT_GRAD_WAVES_C3 8  // C = 3: 64 VGPRs without spills (then 7 workgroups per CU, LDS-bound);
+                              // C = 1 spills at 8, the generic paths are LDS-bound at 5
+#endif
 #ifndef DIRT_GRAD_ATTR
 #define DIRT_GRAD_ATTR
 #endif
@@ -1258,7 +1262,8 @@ __device__ __forceinline__ int run_start(int key, int lx)
 // 32 skip the DPP run scan (every lane adds into LDS), 128 phase timestamps, 256 flush sums without
 // the global atomics
 template <int CC, int AB = 0>
-__global__ __launch_bounds__(256, DIRT_GRAD_WAVES) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
+                          amdgpu_waves_per_eu(CC == 3 ? DIRT_GRAD_WAVES_C3 : DIRT_GRAD_WAVES))) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
                                                    const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
