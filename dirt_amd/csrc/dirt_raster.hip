@@ -137,11 +137,16 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.ntx = (W + kTile - 1) / kTile;
     L.nty = (H + kTile - 1) / kTile;
     L.ntiles = L.ntx * L.nty;
-    L.cshift = (W <= 4096 && H <= 4096) ? 6 : 7;
-    L.csize = 1 << L.cshift;
-    L.nctx = (W + L.csize - 1) >> L.cshift;
-    L.ncty = (H + L.csize - 1) >> L.cshift;
-    L.ncoarse = L.nctx * L.ncty;
+#ifndef DIRT_COARSE_SHIFT
+#define DIRT_COARSE_SHIFT 6  // coarse tile edge 64 px (grown until the frame has <= kMaxCoarse of them)
+#endif
+    for (L.cshift = DIRT_COARSE_SHIFT;; ++L.cshift) {
+        L.csize = 1 << L.cshift;
+        L.nctx = (W + L.csize - 1) >> L.cshift;
+        L.ncty = (H + L.csize - 1) >> L.cshift;
+        L.ncoarse = L.nctx * L.ncty;
+        if (L.ncoarse <= kMaxCoarse) break;
+    }
     L.nrec = (int64_t)(1 + kExtraPerFace) * F;
     const int64_t slabs = std::max<int64_t>((int64_t)B * L.ncoarse, 1);
     L.bin_capacity = bin_capacity > 0 ? bin_capacity : default_capacity(B, F, L.ncoarse);
