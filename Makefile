@@ -7,7 +7,7 @@ CC ?= gcc
 
 # -ffp-contract=off + correctly rounded divide: the raster rules are stated as
 # single IEEE operations so that the HIP path and the oracle agree bit-exactly on coverage and depth.
-# -Wno-pass-failed: the C = 3 backward asks for 8 waves / SIMD (its register budget) although LDS caps it at 7
+# -Wno-pass-failed: the generic-C backward paths ask for 6 waves / SIMD although LDS caps them at 5
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
            -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Wno-pass-failed
 ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall

@@ -1284,8 +1284,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     __shared__ int32_t s_gb[kHaloPix];
     __shared__ uint8_t s_cov[kHaloPix];  // neighbour_coverage() bits of the pixel's face (forward)
     __shared__ int8_t s_slot[kHaloPix];  // slot of the pixel's record, -1 none, kNoSlot table full
-    __shared__ float s_sx[kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), see DESIGN.md 4
-    __shared__ float s_sy[kHaloPix];
+#ifndef DIRT_GRAD_PAIR_RECOMPUTE
+#define DIRT_GRAD_PAIR_RECOMPUTE 1
+#endif
+    // RGB: each lane recomputes the pair scalars of its four pairs in phase B instead of staging them
+    // (LDS 22 -> 19 KiB: 8 workgroups per CU instead of 7); other channel counts stage them in phase A
+    constexpr bool kRecompute = DIRT_GRAD_PAIR_RECOMPUTE && CM == 3;
+    __shared__ float s_sx[kRecompute ? 1 : kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), DESIGN.md 4
+    __shared__ float s_sy[kRecompute ? 1 : kHaloPix];
     // G / I of the staged pixels (phases A-B), then reused for the run-tail partial sums (C-D):
     // keeps the workgroup at ~26 KB of LDS (6 per CU)
     constexpr int kUnion = 2 * kHaloPix * CP;
@@ -1294,6 +1300,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     float *const s_G = s_u;
     float *const s_I = s_u + kHaloPix * CP;
     float *const s_part = s_u;
+    // pair scalar of the pair (klo, klo + x) (axis 0) or (klo, klo + kHalo) (axis 1)
+    auto pair_s = [&](int axis, int klo) -> float {
+        if constexpr (kRecompute)
+            return pair_scalar<CP, CM>(s_gb, s_G, s_I, klo, klo + (axis == 0 ? 1 : kHalo), C);
+        else
+            return axis == 0 ? s_sx[klo] : s_sy[klo];
+    };
     __shared__ SlotTable T;
     // per slot: its number of row runs (= run tails), then the start (a cursor during the tail phase)
     // of its contiguous range of tail partials in s_part
@@ -1425,6 +1438,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         }
         // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
         // bottom row of the halo (their one pair into the tile); nothing reads the others
+        if constexpr (!kRecompute) {
         const int rt = (t & 63) * 4 + (t >> 6);
         s_sx[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + 1, C);
         s_sy[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + kHalo, C);
@@ -1434,6 +1448,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         } else if (rt < 32) {
             const int k = rt - 15;  // (rt - 15, 0)
             s_sy[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + kHalo, C);
+        }
         }
         if (filler) {
             bool small = true;
@@ -1544,7 +1559,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                 const int kq = kme + dj * kHalo + di;
                 const int32_t gq = s_gb[kq];
                 const uint32_t covq = s_cov[kq];  // read unconditionally: the code below is all selects
-                const float s = axis == 0 ? s_sx[me_low ? kme : kq] : s_sy[me_low ? kme : kq];
+                const float s = pair_s(axis, me_low ? kme : kq);
                 const int32_t rq = gq & kGbufIndexMask;
                 int code = 1 + (int)((covq >> (dir ^ 1)) & 1u) - (int)((covme >> dir) & 1u);
                 code = rq == rp ? (me_low ? 2 : 0) : code;
@@ -1581,7 +1596,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             const int32_t gq = s_gb[kq];
             if (gq == -2) continue;
             const int klo = me_low ? kme : kq;
-            const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
+            const float s = pair_s(axis, klo);
             if (s == 0.0f) continue;
             const int32_t rq = gq >= 0 ? (gq & kGbufIndexMask) : -1;
             const int fq = rq >= 0 ? face_of_record(rq, F) : -1;
@@ -1610,7 +1625,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             const bool me_low = (dir & 1) == 0;
             const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
             const int klo = me_low ? kme : kme + dj * kHalo + di;
-            const float s = axis == 0 ? s_sx[klo] : s_sy[klo];
+            const float s = pair_s(axis, klo);
             const float omega = code == 2u ? 1.0f : 0.5f;
             // midpoint: E(p) + E(q) = 2 E(p) + step, step = one pixel (256 sub-pixels) of the edge
             float m[3];
