@@ -1239,8 +1239,9 @@ __device__ __forceinline__ float pair_scalar(const int32_t *s_gb, const float *s
     const int32_t g1 = s_gb[k], g2 = s_gb[k2];
     float a = 0.0f;
     if (CP == 4 && CM == 3) {
-        const float4 Gp = *reinterpret_cast<const float4 *>(&s_G[k * 4]), Gq = *reinterpret_cast<const float4 *>(&s_G[k2 * 4]);
-        const float4 Ip = *reinterpret_cast<const float4 *>(&s_I[k * 4]), Iq = *reinterpret_cast<const float4 *>(&s_I[k2 * 4]);
+        typedef float f3v __attribute__((ext_vector_type(3)));  // ds_read_b96: 3 registers per operand
+        const f3v Gp = *reinterpret_cast<const f3v *>(&s_G[k * 4]), Gq = *reinterpret_cast<const f3v *>(&s_G[k2 * 4]);
+        const f3v Ip = *reinterpret_cast<const f3v *>(&s_I[k * 4]), Iq = *reinterpret_cast<const f3v *>(&s_I[k2 * 4]);
         a = (Gp.x + Gq.x) * (Iq.x - Ip.x);
         a = a + (Gp.y + Gq.y) * (Iq.y - Ip.y);
         a = a + (Gp.z + Gq.z) * (Iq.z - Ip.z);
