@@ -1499,14 +1499,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         const Rec &rr = frame_recs[rp];  // large records and the basis of clipped faces
         const int hx = lx + 1, hy = ly + 1;  // region coordinates of this pixel
         int32_t mA[3], mB[3], eme[3];       // eme: E + owned here (small records only)
-        float iw0, iw1, iw2, w0, w1, w2, h2d;
+        float iw0, iw1, iw2, h2d;
         float fEp[3];
         bool me_small;
         if (sp >= 0) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { mA[k] = T.A[k][sp]; mB[k] = T.B[k][sp]; }
             iw0 = T.iw[0][sp]; iw1 = T.iw[1][sp]; iw2 = T.iw[2][sp];
-            w0 = T.w[0][sp]; w1 = T.w[1][sp]; w2 = T.w[2][sp];
             h2d = T.h2d[sp];
             me_small = !slot_is_large(T, sp);
         } else {
@@ -1514,8 +1513,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
 #pragma unroll
             for (int k = 0; k < 3; ++k) { mA[k] = me.A[k]; mB[k] = me.B[k]; }
             iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
-            const FaceData &fdr = fdata_frame[f];
-            w0 = fdr.w[0]; w1 = fdr.w[1]; w2 = fdr.w[2];
             int64_t E0[3];
             edge_values(me, i, j, E0);
             h2d = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
@@ -1650,6 +1647,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             } else {
                 float lm[3];
                 if (!fast_lambda(rr, multi, m[0], m[1], m[2], lm)) continue;
+                // clip w of the parent vertices, read here (clipped faces only) to keep them out of
+                // the registers of the common path
+                const float w0 = sp >= 0 ? T.w[0][sp] : fdata_frame[f].w[0];
+                const float w1 = sp >= 0 ? T.w[1][sp] : fdata_frame[f].w[1];
+                const float w2 = sp >= 0 ? T.w[2][sp] : fdata_frame[f].w[2];
                 const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
                 if (Wm == 0.0f) continue;
                 const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
