@@ -1496,7 +1496,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         // vector-memory path (L1-resident: a wave touches a handful of records).
         const int f = face_of_record(rp, F);
         const bool multi = (gp & kGbufMulti) != 0;
-        const Rec &rr = frame_recs[rp];  // large records and the basis of clipped faces
+        // the own record (large records and the basis of clipped faces): its address is recomputed at
+        // each use from rp (the asm hides the common subexpression) instead of living in two registers
+        auto rec = [&]() -> const Rec & {
+            int r2 = rp;
+            asm volatile("" : "+v"(r2));
+            return frame_recs[r2];
+        };
         const int hx = lx + 1, hy = ly + 1;  // region coordinates of this pixel
         int32_t mA[3], mB[3], eme[3];       // eme: E + owned here (small records only)
         float iw0, iw1, iw2, h2d;
@@ -1509,6 +1515,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             h2d = T.h2d[sp];
             me_small = !slot_is_large(T, sp);
         } else {
+            const Rec &rr = rec();
             const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
 #pragma unroll
             for (int k = 0; k < 3; ++k) { mA[k] = me.A[k]; mB[k] = me.B[k]; }
@@ -1525,7 +1532,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                 fEp[k] = (float)(eme[k] - owned_bit(mA[k], mB[k]));
             }
         } else {
-            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rec());
             int64_t Ep[3];
             edge_values(me, i, j, Ep);
 #pragma unroll
@@ -1646,7 +1653,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                 for (int k = 0; k < 3; ++k) g[k] = c * m[k];
             } else {
                 float lm[3];
-                if (!fast_lambda(rr, multi, m[0], m[1], m[2], lm)) continue;
+                if (!fast_lambda(rec(), multi, m[0], m[1], m[2], lm)) continue;
                 // clip w of the parent vertices, read here (clipped faces only) to keep them out of
                 // the registers of the common path
                 const float w0 = sp >= 0 ? T.w[0][sp] : fdata_frame[f].w[0];
@@ -1667,7 +1674,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         }
         // colour weights last: keeps their registers out of the pair loop's live range
         float lam[3];
-        if (!(AB & 2) && fast_lambda(rr, multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
+        if (!(AB & 2) && fast_lambda(rec(), multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
             float Gm[CM];
 #pragma unroll
             for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
