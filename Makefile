@@ -8,17 +8,19 @@ CC ?= gcc
 # -ffp-contract=off + correctly rounded divide: the raster rules are stated as
 # single IEEE operations so that the HIP path and the oracle agree bit-exactly on coverage and depth.
 # -amdgpu-set-wave-priority: waves raise their priority (s_setprio) while issuing their loads, so the
-# latency-bound setup/raster/grad waves get their memory requests out before VALU-heavy neighbours
-# (A/B on one box, two rounds: 16.0 -> 16.4-16.7 Gpixels/s).
+# latency-bound setup/raster/grad waves get their memory requests out before VALU-heavy neighbours.
+# A/B on one box, three interleaved rounds (profiles/r02/ab_waveprio_*): without 16.06 / 16.10 / 15.96,
+# with 16.59 / 16.49 / 16.40 Gpixels/s (+2.8 %).  `make WAVEPRIO=` builds without it.
 # -Wno-pass-failed: the generic-C backward paths ask for 6 waves / SIMD although LDS caps them at 5
+WAVEPRIO ?= -mllvm -amdgpu-set-wave-priority
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-           -fhip-fp32-correctly-rounded-divide-sqrt -mllvm -amdgpu-set-wave-priority -Wall -Wno-unused-function -Wno-pass-failed
+           -fhip-fp32-correctly-rounded-divide-sqrt $(WAVEPRIO) -Wall -Wno-unused-function -Wno-pass-failed
 ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall
 
 LIB = dirt_amd/libdirt_mi355x.so
 ORACLE = oracle/libdirt_oracle.so
 HIP_SRC = dirt_amd/csrc/dirt_raster.hip
-HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h include/dirt_mi355x.h
+HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h
 
 all: $(LIB) $(ORACLE)
 

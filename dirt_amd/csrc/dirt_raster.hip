@@ -808,14 +808,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         // accumulators if it passed them (after the slab loads are in flight)
         const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
         const int64_t gt = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x, gs = nblk * 256;
+        // (16-B stores where the caller's buffer is 16-B aligned -- torch allocations are -- else scalar)
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (zero_a) {
-            for (int64_t k = gt; k < (nzero_a >> 2); k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
-            for (int64_t k = (nzero_a & ~3LL) + gt; k < nzero_a; k += gs) zero_a[k] = 0.f;
+            const int64_t n4 = (reinterpret_cast<uintptr_t>(zero_a) & 15) == 0 ? (nzero_a >> 2) : 0;
+            for (int64_t k = gt; k < n4; k += gs) reinterpret_cast<float4 *>(zero_a)[k] = z4;
+            for (int64_t k = 4 * n4 + gt; k < nzero_a; k += gs) zero_a[k] = 0.f;
         }
         if (zero_b) {
-            for (int64_t k = gt; k < (nzero_b >> 2); k += gs) reinterpret_cast<float4 *>(zero_b)[k] = z4;
-            for (int64_t k = (nzero_b & ~3LL) + gt; k < nzero_b; k += gs) zero_b[k] = 0.f;
+            const int64_t n4 = (reinterpret_cast<uintptr_t>(zero_b) & 15) == 0 ? (nzero_b >> 2) : 0;
+            for (int64_t k = gt; k < n4; k += gs) reinterpret_cast<float4 *>(zero_b)[k] = z4;
+            for (int64_t k = 4 * n4 + gt; k < nzero_b; k += gs) zero_b[k] = 0.f;
         }
     }
     // an overflowed slab (more pairs than its capacity): filter every record of the frame instead
@@ -1790,17 +1793,14 @@ __global__ __launch_bounds__(256) void zero2_kernel(float *__restrict__ a, int64
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // a is 16-B aligned (torch / caller allocations); vector part then tail
-    const int64_t na4 = na / 4, nb4 = nb / 4;
+    // 16-B stores over a 16-B aligned buffer (torch allocations), scalar stores otherwise; then the tail
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t na4 = (reinterpret_cast<uintptr_t>(a) & 15) == 0 ? na / 4 : 0;
+    const int64_t nb4 = (reinterpret_cast<uintptr_t>(b) & 15) == 0 ? nb / 4 : 0;
     for (int64_t k = gid; k < na4; k += stride) reinterpret_cast<float4 *>(a)[k] = z;
     for (int64_t k = na4 * 4 + gid; k < na; k += stride) a[k] = 0.0f;
-    if ((reinterpret_cast<uintptr_t>(b) & 15) == 0) {
-        for (int64_t k = gid; k < nb4; k += stride) reinterpret_cast<float4 *>(b)[k] = z;
-        for (int64_t k = nb4 * 4 + gid; k < nb; k += stride) b[k] = 0.0f;
-    } else {
-        for (int64_t k = gid; k < nb; k += stride) b[k] = 0.0f;
-    }
+    for (int64_t k = gid; k < nb4; k += stride) reinterpret_cast<float4 *>(b)[k] = z;
+    for (int64_t k = nb4 * 4 + gid; k < nb; k += stride) b[k] = 0.0f;
 }
 
 // PMC calibration (tools/pmc_calibrate.py): read `n` elements of W bytes once each, coalesced, with the

@@ -8,7 +8,10 @@ libdirt_mi355x.so, and the op gets the gradient the reference never registered (
 Differences from the reference, all deliberate:
   * `camera_pos` is optional (default None): the fork made it a mandatory positional argument of
     `rasterise` (rasterise_ops.py:10) but forgot it in `rasterise_batch` (:84-88), so every
-    upstream-style caller raised; here both call forms work.
+    upstream-style caller raised; here both call forms work, positional ones included: an integer in the
+    camera_pos slot is upstream DIRT's `height` (upstream signature `(background, vertices,
+    vertex_colors, faces, height=None, width=None, channels=None, name=None)`), so the remaining
+    positional arguments shift by one (`_upstream_positional`).
   * channels may be 1..8 (the reference CHECK-aborts unless 1 or 3, csrc/hwc.h:27), so the 7-channel
     deferred G-buffer (BASELINE config 4) is one call instead of three.
   * errors are exceptions, never process aborts (csrc/rasterise_egl.cpp:85-503 LOG(FATAL)).
@@ -118,6 +121,15 @@ _CAMERA_FLOATS = {
 }
 
 
+def _upstream_positional(camera_pos, height, width, channels, name):
+    """Upstream DIRT has no camera_pos: `rasterise(bg, v, c, f, H, W, C)` binds H to our camera_pos slot.
+    An integer there (a camera position is a float tensor / sequence, never a Python int) is that height;
+    shift height / width / channels / name back into place."""
+    if isinstance(camera_pos, (int, np.integer)) and not isinstance(camera_pos, bool):
+        return None, int(camera_pos), height, width, channels
+    return camera_pos, height, width, channels, name
+
+
 def _camera(camera_pos, shader_id, dev):
     if camera_pos is None:
         if shader_id != _lib.SHADER_GOURAUD:
@@ -186,6 +198,7 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
     Returns:
         float32 [height, width, channels] pixels, differentiable w.r.t. background, vertices, vertex_colors.
     """
+    camera_pos, height, width, channels, name = _upstream_positional(camera_pos, height, width, channels, name)
     del name
     bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
     if height is None:
@@ -210,6 +223,7 @@ def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None,
     Conceptually `torch.stack([rasterise(bg_i, v_i, c_i, f_i) for ...])`; every argument carries a leading
     batch dimension and faces index the vertices of their own frame.
     """
+    camera_pos, height, width, channels, name = _upstream_positional(camera_pos, height, width, channels, name)
     del name
     bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
     if height is None:

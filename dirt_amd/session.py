@@ -42,15 +42,33 @@ class RasteriseSession:
             raise ValueError("RasteriseSession expects a contiguous %s %s tensor on %s, got %s %s on %s"
                              % (dtype, shape, self.device, t.dtype, tuple(t.shape), t.device))
 
+    def _check_camera(self, camera_pos):
+        """camera_pos as rasterise_ops._camera requires it, without copies: a contiguous float32 tensor on
+        this device holding at least the floats the fragment program reads (its pointer goes straight to
+        the kernel).  Returns the device pointer, or None for Gouraud without a camera."""
+        from .rasterise_ops import _CAMERA_FLOATS
+        if camera_pos is None:
+            if self.shader_id != _lib.SHADER_GOURAUD:
+                raise ValueError("procedural fragment programs need camera_pos (8 floats)")
+            return None
+        need, why = _CAMERA_FLOATS.get(self.shader_id, (8, "camera_pos must hold at least 8 floats "
+                                                           "(csrc/rasterise_egl.cpp:323)"))
+        if (not isinstance(camera_pos, torch.Tensor) or camera_pos.device != self.device
+                or camera_pos.dtype != torch.float32 or not camera_pos.is_contiguous()):
+            raise ValueError("RasteriseSession expects camera_pos as a contiguous float32 tensor on %s" % self.device)
+        if camera_pos.numel() < need:
+            raise ValueError(why or "camera_pos must hold at least %d floats" % need)
+        return camera_pos.data_ptr()
+
     def forward(self, background, vertices, vertex_colors, faces, camera_pos=None):
         B, H, W, C, V, F = self.dims
         self._check(background, (B, H, W, C), torch.float32)
         self._check(vertices, (B, V, 4), torch.float32)
         self._check(vertex_colors, (B, V, C), torch.float32)
         self._check(faces, (B, F, 3), torch.int32)
+        cam = self._check_camera(camera_pos)
         self._inputs = (background, vertices, vertex_colors, faces)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        cam = camera_pos.data_ptr() if camera_pos is not None else None
         _lib.check(self._lib.dirt_rasterise_fwd(
             background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
             B, H, W, C, V, F, self.shader_id, self.pixels.data_ptr(), self.gbuffer.data_ptr(),
@@ -62,6 +80,8 @@ class RasteriseSession:
     def backward(self, grad_pixels):
         if self._inputs is None:
             raise RuntimeError("RasteriseSession.backward called before forward")
+        if self.shader_id != _lib.SHADER_GOURAUD:
+            raise RuntimeError("only the Gouraud fragment program has a gradient (the reference registers none)")
         B, H, W, C, V, F = self.dims
         self._check(grad_pixels, (B, H, W, C), torch.float32)
         _, vertices, vertex_colors, faces = self._inputs

@@ -107,7 +107,10 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
 #define DIRT_FWD_SCRATCH_CLEAN 1u /* the scratch is clean: skip the forward's own clearing memset */
 /* zero_grad_vertices [B,V,4] / zero_grad_vertex_colors [B,V,C] (each may be NULL): accumulators the
  * forward zero-fills in passing (inside its raster kernel), for a later dirt_rasterise_bwd with
- * DIRT_BWD_ACCUMULATE -- a fixed-shape training loop then pays no separate clearing launch. */
+ * DIRT_BWD_ACCUMULATE -- a fixed-shape training loop then pays no separate clearing launch.
+ * Alignment: no pointer argument of this ABI needs more than its element's natural alignment (4 B);
+ * 16-B aligned buffers (every torch / hipMalloc allocation) take the vectorised zero-fill path, others
+ * (views at an offset) a scalar one. */
 
 /* Backward: given grad_pixels = dL/dpixels, writes dL/dvertices [B,V,4] (z component is 0),
  * dL/dvertex_colors [B,V,C] and dL/dbackground [B,H,W,C].  All three outputs are fully

@@ -103,3 +103,20 @@ def test_lighting_helpers():
     assert p.shape == (6, 3) and float(p.min()) >= 0
     sp = lighting.specular_directional(sv, n, torch.ones(6, 3), [0., 0., -1.], [1., 1., 1.], [0., 0., 3.], 6.0)
     assert sp.shape == (6, 3)
+
+
+def test_upstream_positional_call_form():
+    # upstream DIRT: rasterise_batch(background, vertices, vertex_colors, faces, height, width, channels, name)
+    # binds height to the fork's camera_pos slot; an integer there shifts the rest back into place
+    up = rasterise_ops._upstream_positional
+    assert up(48, 64, 3, None, None) == (None, 48, 64, 3, None)
+    assert up(np.int64(48), 64, 3, "nm", None) == (None, 48, 64, 3, "nm")
+    cam = [0.0] * 8
+    assert up(cam, 48, 64, 3, None) == (cam, 48, 64, 3, None)
+    assert up(None, None, None, None, None) == (None, None, None, None, None)
+    if not torch.cuda.is_available():
+        # the positional upstream call reaches the device check, not a camera_pos error
+        bg = np.zeros((1, 8, 8, 3), np.float32)
+        with pytest.raises(RuntimeError, match="GPU"):
+            dirt_amd.rasterise_batch(bg, np.zeros((1, 3, 4), np.float32), np.zeros((1, 3, 3), np.float32),
+                                     np.zeros((1, 1, 3), np.int32), 8, 8, 3)

@@ -297,3 +297,62 @@ def test_large_triangle_stress_r64():
     """SURVEY 8d stress variant (r = 64 px) at full 1024^2 with fewer faces: big bins, records spanning
     many coarse tiles (workgroup-cooperative binning), large-edge records in the backward."""
     check_scene(*scenes.random_triangles(F=4000, W=1024, H=1024, radius_px=64.0, seed=6))
+
+
+def test_session_argument_checks():
+    # camera_pos must be a device float32 tensor with the floats the program reads; a procedural
+    # session has no gradient (ADVICE r1: the session checked less than the autograd path)
+    from dirt_amd.session import RasteriseSession
+    bg, v, c, f = scenes.random_triangles(F=40, W=32, H=24, C=3, seed=3)
+    t = [_gpu(a[None]) for a in (bg, v, c, f)]
+    sess = RasteriseSession(1, 24, 32, 3, v.shape[0], f.shape[0], shader_id=1)
+    with pytest.raises(ValueError, match="camera_pos"):
+        sess.forward(*t)
+    with pytest.raises(ValueError, match="camera_pos"):
+        sess.forward(*t, camera_pos=torch.zeros(8))  # host tensor
+    with pytest.raises(ValueError, match="camera_pos"):
+        sess.forward(*t, camera_pos=torch.zeros(8, dtype=torch.float64, device="cuda"))
+    with pytest.raises(ValueError, match="8"):
+        sess.forward(*t, camera_pos=torch.zeros(7, device="cuda"))
+    sess.forward(*t, camera_pos=torch.zeros(8, device="cuda"))
+    with pytest.raises(RuntimeError, match="gradient"):
+        sess.backward(torch.zeros_like(t[0]))
+    hill = RasteriseSession(1, 24, 32, 3, v.shape[0], f.shape[0], shader_id=7)
+    with pytest.raises(ValueError, match="12"):
+        hill.forward(*t, camera_pos=torch.zeros(8, device="cuda"))
+
+
+def test_upstream_positional_rasterise_batch_on_gpu():
+    import dirt_amd
+    bg, v, c, f = scenes.random_triangles(F=60, W=40, H=32, C=3, seed=5)
+    ref = dirt_amd.rasterise_batch(_gpu(bg[None]), _gpu(v[None]), _gpu(c[None]), _gpu(f[None]),
+                                   height=32, width=40, channels=3)
+    pos = dirt_amd.rasterise_batch(_gpu(bg[None]), _gpu(v[None]), _gpu(c[None]), _gpu(f[None]), 32, 40, 3)
+    one = dirt_amd.rasterise(_gpu(bg), _gpu(v), _gpu(c), _gpu(f), 32, 40, 3)
+    torch.testing.assert_close(pos, ref, rtol=0, atol=0)
+    torch.testing.assert_close(one, ref[0], rtol=0, atol=0)
+
+
+def test_forward_zero_fill_of_misaligned_accumulators():
+    # zero_grad_* views at a 4-byte offset (not 16-B aligned) take the scalar zero-fill; the guard
+    # elements either side stay untouched
+    from dirt_amd import _lib
+    bg, v, c, f = scenes.random_triangles(F=50, W=32, H=32, C=3, seed=7)
+    B, H, W, C, V, F = 1, 32, 32, 3, v.shape[0], f.shape[0]
+    t = [_gpu(a[None]) for a in (bg, v, c, f)]
+    saved_b, scratch_b = _lib.workspace_sizes(B, H, W, C, V, F)
+    saved = torch.empty(saved_b, dtype=torch.uint8, device="cuda")
+    scratch = torch.zeros(scratch_b, dtype=torch.uint8, device="cuda")
+    px = torch.empty((B, H, W, C), device="cuda")
+    gb = torch.empty((B, H, W), dtype=torch.int32, device="cuda")
+    ga = torch.full((B * V * 4 + 2,), 7.0, device="cuda")
+    gc = torch.full((B * V * C + 2,), 7.0, device="cuda")
+    lib = _lib.load()
+    _lib.check(lib.dirt_rasterise_fwd(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), None,
+                                      B, H, W, C, V, F, 0, px.data_ptr(), gb.data_ptr(), saved.data_ptr(), saved_b,
+                                      scratch.data_ptr(), scratch_b, 0, 0, ga[1:].data_ptr(), gc[1:].data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    for a in (ga, gc):
+        h = a.cpu().numpy()
+        assert h[0] == 7.0 and h[-1] == 7.0 and np.all(h[1:-1] == 0.0)
