@@ -518,6 +518,10 @@ __device__ __forceinline__ int xcd_tile(int x, int n)
     return g * q + min(g, r) + k;
 }
 
+#ifndef DIRT_RASTER_LISTS
+#define DIRT_RASTER_LISTS 1  // per-wave entry lists (1) or the scalar bit-mask walk (0)
+#endif
+constexpr int kWaveList = 256 + 2;  // a staging round's entries + the even pad
 constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per wave and chunk (2 loads per lane in flight)
 // A staged record is "small" when every |A|, |B| < 2^15: its edge steps inside a strip are one
 // v_dot2_i32_i16 of the packed (A, B) with the lane's packed (dx, dy) offsets (<= 15*256, 3*256).
@@ -635,6 +639,19 @@ __device__ __forceinline__ EntryRegs load_entry(const StripEntry *ent, int e)
 {
     lds_int4v *ve = (lds_int4v *)(ent) + 3 * e;
     return EntryRegs{ve[0], ve[1], ve[2]};
+}
+
+// the same at a byte offset into the staging array (a per-wave list element)
+__device__ __forceinline__ EntryRegs load_entry_at(const StripEntry *ent, uint32_t off)
+{
+    lds_int4v *ve = (lds_int4v *)((const char *)ent + off);
+    return EntryRegs{ve[0], ve[1], ve[2]};
+}
+
+// rank of this lane among the set lanes of `mask` below it
+__device__ __forceinline__ int lane_rank(uint64_t mask)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 template <bool NoDepth, bool Large>
@@ -760,8 +777,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const int C = CC > 0 ? CC : Cdyn;
     __shared__ int32_t t_list[kStrips][kFilterBlock];  // per-wave segments of the tile's survivors
     __shared__ int32_t t_nw[2][kStrips];                // segment lengths, double-buffered by chunk parity
-    __shared__ StripEntry t_ent[256];                   // one staging round: an entry per thread
+    __shared__ StripEntry t_ent[257];                   // one staging round: an entry per thread (+ sentinel)
     __shared__ uint8_t t_mask[256];                     // strips the entry can cover; bit 4: large
+#if DIRT_RASTER_LISTS
+    // per-wave entry lists of a staging round: byte offsets into t_ent of the small entries from the
+    // front (padded to even with the sentinel), indices of the large ones from the back
+    __shared__ uint32_t t_wl[kStrips][kWaveList];
+    if (threadIdx.x == 0) {
+        // sentinel t_ent[256]: ab = 0 so every edge value stays -2^30 (never covers)
+        int4 *d = reinterpret_cast<int4 *>(&t_ent[256]);
+        d[0] = make_int4(-(1 << 30), -(1 << 30), -(1 << 30), 0);
+        d[1] = make_int4(0, 0, 0, 0);
+        d[2] = make_int4(0, 0, 0, 0);
+    }
+#endif
     // Gouraud: XCD bands (L2 sharing of bins / records between neighbouring tiles); a procedural
     // program is compute-bound and its cost follows the image content (sky vs water), so its tiles are
     // interleaved over the XCDs instead (round-robin dispatch order) for balance
@@ -907,6 +936,40 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                 __syncthreads();
                 if (chunk == 0 && from == 0) PHASE_TS(2);
                 const int nst = min(256, n_list - from);
+#if DIRT_RASTER_LISTS
+                if (!(AB & 1)) {
+                    // this wave's entries as a list (ballot compaction of the round's masks): the loop then
+                    // walks offsets read two at a time instead of scanning a bit mask on the scalar unit
+                    int ns = 0, nl = 0;
+                    for (int c0 = 0; c0 < nst; c0 += 64) {
+                        const uint32_t mm = c0 + lane < nst ? t_mask[c0 + lane] : 0u;
+                        const bool mine = (mm >> wave) & 1u, big = (mm >> 4) & 1u;
+                        const uint64_t bs = __ballot(mine && !big), bl = __ballot(mine && big);
+                        if (mine && !big) t_wl[wave][ns + lane_rank(bs)] = (uint32_t)(c0 + lane) * sizeof(StripEntry);
+                        if (mine && big) t_wl[wave][kWaveList - 1 - (nl + lane_rank(bl))] = (uint32_t)(c0 + lane);
+                        ns += __popcll(bs);
+                        nl += __popcll(bl);
+                    }
+                    if (lane == 0 && (ns & 1)) t_wl[wave][ns] = 256u * sizeof(StripEntry);
+                    wave_lds_sync();
+                    // two entries per iteration; the next pair's offsets are read before this pair is
+                    // tested (reads at k + 2 <= ns + 1 stay inside the list)
+                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                    typedef const volatile __attribute__((address_space(3))) u32x2 lds_u32x2;
+                    u32x2 oo = *(lds_u32x2 *)&t_wl[wave][0];
+                    for (int k = 0; k < ns; k += 2) {
+                        const EntryRegs qa = load_entry_at(t_ent, oo.x), qb = load_entry_at(t_ent, oo.y);
+                        oo = *(lds_u32x2 *)&t_wl[wave][k + 2];
+                        raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, i, j, best);
+                        raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, i, j, best);
+                    }
+                    for (int k = 0; k < nl; ++k)
+                        raster_entry<kNoDepth, true>(load_entry(t_ent, (int)t_wl[wave][kWaveList - 1 - k]), frame_recs, pix,
+                                                     pxy, i, j, best);
+                } else if (nst > 0) {
+                    best += t_ent[lane % nst].key;
+                }
+#else
                 if (!(AB & 1)) {
                     for (int c0 = 0; c0 < nst; c0 += 64) {
                         const uint32_t mm = c0 + lane < nst ? t_mask[c0 + lane] : 0u;
@@ -942,6 +1005,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                 } else if (nst > 0) {
                     best += t_ent[lane % nst].key;
                 }
+#endif
                 // t_ent / t_mask are rewritten by the next round of this chunk; a next chunk rewrites
                 // them only after its own filter barrier, and the last round needs no barrier at all
                 if (from + 256 < n_list) __syncthreads();
