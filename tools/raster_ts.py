@@ -37,7 +37,7 @@ def main():
     rd.argtypes = [P, ctypes.c_int]
     stream = torch.cuda.current_stream().cuda_stream
     ms = ctypes.c_float(0)
-    nwg = ((W + 15) // 16) * ((H + 15) // 16) * B
+    nwg = ((W + 15) // 16) * ((H + 15) // 16) * B  # raster tiles are 16 x 16
     for variant in (0, 128, 0, 128):
         _lib.check(rfn(variant, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), B, H, W, C, V, F,
                        sess.pixels.data_ptr(), sess.gbuffer.data_ptr(), sess.saved.data_ptr(), sess.scratch.data_ptr(),
@@ -69,6 +69,15 @@ def main():
     life = T[:, 5] - T[:, 0]
     print("  %-22s median %8.0f  p90 %8.0f  mean %8.0f ticks  (%.2f us)" % (
         "workgroup life", np.median(life), np.percentile(life, 90), life.mean(), life.mean() * tick_us))
+    # dispatch: workgroups per CU and how late they started (rebased per CU)
+    cnt = np.bincount(key)
+    cnt = cnt[cnt > 0]
+    late = T[:, 0] > 0.25 * span
+    print("  WGs per CU: min %d median %d max %d; started after 25%% of the span: %d of %d" % (
+        cnt.min(), np.median(cnt), cnt.max(), late.sum(), len(late)))
+    for q in (10, 50, 90, 99):
+        print("  start p%d %.2f us, end p%d %.2f us" % (q, np.percentile(T[:, 0], q) * tick_us, q,
+                                                    np.percentile(T[:, 5], q) * tick_us))
 
 
 if __name__ == "__main__":
