@@ -123,6 +123,12 @@ constexpr int64_t kDefaultBinBudget = 1ll << 27;  // entries (1 GiB) above which
 // other set being zero) and publishes Q = P ^ 1 for the next forward.  Each word is only read by one kernel and only written (one workgroup,
 // one value) by the other, so no launch reads a word it writes.  Zeroed scratch = a valid state.
 constexpr int kParP = 16, kParQ = 32;
+// Words between two bin counters: the setup's reservation atomics execute at the memory side, and ~200
+// workgroups reserving in the same few lines serialise there, so every counter gets a line of its own.
+#ifndef DIRT_COUNT_STRIDE
+#define DIRT_COUNT_STRIDE 64
+#endif
+constexpr int kCountStride = DIRT_COUNT_STRIDE;
 
 int64_t default_capacity(int B, int F, int ncoarse)
 {
@@ -158,7 +164,7 @@ int make_layout(int B, int H, int W, int F, int64_t bin_capacity, Layout &L)
     L.saved_total = L.saved_cov + (size_t)align_up((int64_t)B * H * W, 256);  // 4 coverage bits per pixel
     const int64_t nc = (int64_t)B * L.ncoarse;
     size_t o = 0;
-    L.off_count = o;  o += (size_t)align_up(2 * nc * 4, 256);  // counts[2][B][ncoarse]
+    L.off_count = o;  o += (size_t)align_up(2 * nc * 4 * kCountStride, 256);  // counts[2][B][ncoarse] (strided)
     L.off_flag = o;   o += 256;
     L.off_bins = o;   o += (size_t)align_up(L.bin_capacity * 8, 256);
     L.scratch_total = o;
@@ -364,13 +370,13 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     PHASE_TS(0);
     const int64_t ncount = (int64_t)B * ncoarse;
     const uint32_t par = flag[kParQ] & 1u;
-    uint32_t *ccount = counts + par * ncount;
+    uint32_t *ccount = counts + par * ncount * kCountStride;
     {
         // publish this forward's parity for the raster; zero the other count set for the next forward
         const int64_t g = (int64_t)blockIdx.y * gridDim.x + blockIdx.x, ng = (int64_t)gridDim.x * gridDim.y;
         if (g == 0 && t == 0) flag[kParP] = par;
-        uint32_t *other = counts + (par ^ 1u) * ncount;
-        for (int64_t k = g * kBinThreads + t; k < ncount; k += ng * kBinThreads) other[k] = 0;
+        uint32_t *other = counts + (par ^ 1u) * ncount * kCountStride;
+        for (int64_t k = g * kBinThreads + t; k < ncount; k += ng * kBinThreads) other[k * kCountStride] = 0;
     }
     for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
     if (t == 0) Q.n = 0;
@@ -452,10 +458,10 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     PHASE_TS(2);
     // reserve this workgroup's range of every touched slab: one returning device atomic per (workgroup,
     // coarse tile), all in flight together
-    uint32_t *cc = ccount + (int64_t)b * ncoarse;
+    uint32_t *cc = ccount + (int64_t)b * ncoarse * kCountStride;
     for (int c = t; c < ncoarse; c += kBinThreads) {
         const uint32_t n = hist[c];
-        base[c] = (AB & 1) ? 0u : n ? atomicAdd(&cc[c], n) : 0u;  // (AB & 1: ablation, no reservation)
+        base[c] = (AB & 1) ? 0u : n ? atomicAdd(&cc[c * kCountStride], n) : 0u;  // (AB & 1: ablation, no reservation)
         hist[c] = 0;
     }
     __syncthreads();
@@ -482,6 +488,24 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         __syncthreads();
         PHASE_TS(7);
     }
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    // LDS ops of one wave execute in order; this only stops the compiler from reordering across it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// launch the setup (and binning) of B frames x F faces
+template <int AB = 0>
+void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F, const Layout &L,
+                  Rec *recs, FaceData *fdata, uint32_t *ccount, uint32_t *flag, uint2 *bins, hipStream_t stream)
+{
+    const dim3 grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
+    setup_kernel<AB><<<grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse,
+                                                             L.nrec, recs, fdata, ccount, flag, bins, L.slab, B);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -572,14 +596,6 @@ __device__ __forceinline__ void depth_update(const Rec &r, uint32_t key, float f
     const uint64_t k = depth_key<NoDepth>(depth_q24(zc), key);
     const bool win = in && zc == zw && k < best;
     best = win ? k : best;
-}
-
-__device__ __forceinline__ void wave_lds_sync()
-{
-    // LDS ops of one wave execute in order; this only stops the compiler from reordering across it
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Stage one tile survivor (record ri) for the 16x16 tile at pixel (ti0, tj0): edge values at the tile
@@ -830,7 +846,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     if (slab > 0 && !(AB & 8)) load_chunk(0);
     // This forward's setup zeroed the other count set, so the count is the sum of both (no dependent
     // parity load); F == 0: setup did not run
-    const uint32_t raw = F > 0 ? counts[cc] + counts[(int64_t)B * ncoarse + cc] : 0u;
+    const uint32_t raw = F > 0 ? counts[cc * kCountStride] + counts[((int64_t)B * ncoarse + cc) * kCountStride] : 0u;
     if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
     if (!(AB & 16)) {
         // housekeeping spread over all blocks (a few KB each): zero-fill the caller's gradient
@@ -1958,12 +1974,9 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     // count sets and parity words: one memset, unless the caller vouches that the scratch is clean
     // (DIRT_FWD_SCRATCH_CLEAN: zeroed once and since used only by forwards of the same layout)
     if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
-    const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     if (F > 0) {
         ProfScope ps(K_SETUP, stream);
-        setup_kernel<0><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
-                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
-                                                                 L.slab, B);
+        launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream);
         HIP_TRY(hipGetLastError());
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
@@ -2096,11 +2109,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
     uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
     // re-bin from a clean scratch, then time the raster variant alone
     HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
-    const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
-    if (F > 0)
-        setup_kernel<0><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx,
-                                                                 L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins,
-                                                                 L.slab, B);
+    if (F > 0) launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream);
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -2146,7 +2155,6 @@ int dirt_debug_setup_ts(int variant, const float *vertices, const int32_t *faces
     uint32_t *flag = reinterpret_cast<uint32_t *>(sc + L.off_flag);
     uint2 *bins = reinterpret_cast<uint2 *>(sc + L.off_bins);
     HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
-    const dim3 bin_grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -2154,9 +2162,7 @@ int dirt_debug_setup_ts(int variant, const float *vertices, const int32_t *faces
     switch (variant) {
 #define V_SETUP(K, AB)                                                                                        \
     case K:                                                                                                   \
-        setup_kernel<AB><<<bin_grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift,      \
-                                                                     L.nctx, L.ncoarse, L.nrec, recs, fdata,     \
-                                                                     ccount, flag, bins, L.slab, B);            \
+        launch_setup<AB>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream);         \
         break
         V_SETUP(0, 128); V_SETUP(1, 129); V_SETUP(2, 0); V_SETUP(3, 1);
 #undef V_SETUP
