@@ -352,6 +352,29 @@ __device__ __forceinline__ uint32_t rel_bbox(uint32_t bx, uint32_t by, int cx, i
     return (uint32_t)a0 | ((uint32_t)a1 << 8) | ((uint32_t)b0 << 16) | ((uint32_t)b1 << 24);
 }
 
+// Zero-fill of two float arrays by a range of workgroups (16-B stores where the buffer is 16-B aligned --
+// torch allocations are -- else scalar)
+struct ZeroFill {
+    float *a, *b;
+    int64_t na, nb;
+    int nfb;  // workgroups before the fillers (blockIdx.x < nfb do the kernel's own work)
+    __device__ void run(int64_t blk, int64_t nblk) const
+    {
+        const int64_t gt = blk * blockDim.x + threadIdx.x, gs = nblk * blockDim.x;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a) {
+            const int64_t n4 = (reinterpret_cast<uintptr_t>(a) & 15) == 0 ? (na >> 2) : 0;
+            for (int64_t k = gt; k < n4; k += gs) reinterpret_cast<float4 *>(a)[k] = z4;
+            for (int64_t k = 4 * n4 + gt; k < na; k += gs) a[k] = 0.f;
+        }
+        if (b) {
+            const int64_t n4 = (reinterpret_cast<uintptr_t>(b) & 15) == 0 ? (nb >> 2) : 0;
+            for (int64_t k = gt; k < n4; k += gs) reinterpret_cast<float4 *>(b)[k] = z4;
+            for (int64_t k = 4 * n4 + gt; k < nb; k += gs) b[k] = 0.f;
+        }
+    }
+};
+
 // K1: setup + coarse binning.  Bin entry = {record index, bbox clamped to the coarse tile, 8 bits per
 // side}; order inside a slab is irrelevant (the depth resolve is a commutative min).
 // AB & 128: per-workgroup phase timestamps (dirt_debug_setup_ts, tools/setup_ts.py)
@@ -361,8 +384,15 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
                                                             int H, int cshift, int nctx, int ncoarse, int64_t nrec,
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
                                                             uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
-                                                            uint2 *__restrict__ bins, uint32_t slab, int B)
+                                                            uint2 *__restrict__ bins, uint32_t slab, int B,
+                                                            const ZeroFill zf)
 {
+    // workgroups past the faces zero-fill the caller's gradient accumulators (DIRT_FWD zero_grad_*): the
+    // setup grid leaves most CUs idle (196 workgroups at config 3), so the fill costs the raster nothing
+    if ((int)blockIdx.x >= zf.nfb) {
+        zf.run((int64_t)blockIdx.y * (gridDim.x - zf.nfb) + (blockIdx.x - zf.nfb), (int64_t)(gridDim.x - zf.nfb) * gridDim.y);
+        return;
+    }
     __shared__ uint32_t hist[kMaxCoarse];
     __shared__ uint32_t base[kMaxCoarse];
     __shared__ BigQueue Q;
@@ -373,7 +403,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     uint32_t *ccount = counts + par * ncount * kCountStride;
     {
         // publish this forward's parity for the raster; zero the other count set for the next forward
-        const int64_t g = (int64_t)blockIdx.y * gridDim.x + blockIdx.x, ng = (int64_t)gridDim.x * gridDim.y;
+        const int64_t g = (int64_t)blockIdx.y * zf.nfb + blockIdx.x, ng = (int64_t)zf.nfb * gridDim.y;  // face workgroups
         if (g == 0 && t == 0) flag[kParP] = par;
         uint32_t *other = counts + (par ^ 1u) * ncount * kCountStride;
         for (int64_t k = g * kBinThreads + t; k < ncount; k += ng * kBinThreads) other[k * kCountStride] = 0;
@@ -501,11 +531,16 @@ __device__ __forceinline__ void wave_lds_sync()
 // launch the setup (and binning) of B frames x F faces
 template <int AB = 0>
 void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F, const Layout &L,
-                  Rec *recs, FaceData *fdata, uint32_t *ccount, uint32_t *flag, uint2 *bins, hipStream_t stream)
+                  Rec *recs, FaceData *fdata, uint32_t *ccount, uint32_t *flag, uint2 *bins, hipStream_t stream,
+                  float *zero_a = nullptr, int64_t nzero_a = 0, float *zero_b = nullptr, int64_t nzero_b = 0)
 {
-    const dim3 grid((unsigned)((F + kFacesPerBlock - 1) / kFacesPerBlock), (unsigned)B);
+    ZeroFill zf{zero_a, zero_b, zero_a ? nzero_a : 0, zero_b ? nzero_b : 0, (F + kFacesPerBlock - 1) / kFacesPerBlock};
+    // filler workgroups per frame row: ~16 float4 stores per thread, at most 64 in all
+    const int64_t z4 = (zf.na + zf.nb) / 4, want = std::min<int64_t>((z4 + 4095) / 4096, 64);
+    const int nzb = z4 > 0 ? (int)std::max<int64_t>(1, (want + B - 1) / B) : 0;
+    const dim3 grid((unsigned)(zf.nfb + nzb), (unsigned)B);
     setup_kernel<AB><<<grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse,
-                                                             L.nrec, recs, fdata, ccount, flag, bins, L.slab, B);
+                                                             L.nrec, recs, fdata, ccount, flag, bins, L.slab, B, zf);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -556,8 +591,10 @@ struct alignas(16) StripEntry {  // 48 B of wave-private LDS per staged (sub-)tr
     int32_t e[3];    // small: E + owned at the strip origin (2^30 when the edge holds over the whole strip);
                      // large: e[0] = record index
     uint32_t ab[3];  // small: (uint16)A | B << 16; large: ab[0] = kLargeAB
-    float za, zb, fx0, fy0, z0;  // fx0, fy0 8-byte aligned: one register pair for v_pk_add_f32
-    uint32_t key;    // face << 3 | sub-triangle: the low word of the depth key (the lower face wins ties)
+    float za, zb, fx0, fy0;  // fx0, fy0 8-byte aligned: one register pair for v_pk_add_f32
+    uint32_t key;    // face << 3 | sub-triangle: the low word of the depth key (the lower face wins ties);
+                     // an even register once loaded, so the quantised depth lands beside it (no move)
+    float z0;
 };
 static_assert(sizeof(StripEntry) == 48, "StripEntry must be 48 B");
 
@@ -689,13 +726,24 @@ __device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__re
         edge_values(r, i, j, E);
         in = inside(r, E);
     }
-    // R4 without branches: in range iff the clamp leaves zw unchanged (false for NaN)
     const float2v d = pxy - float2v{__int_as_float(q.q2.x), __int_as_float(q.q2.y)};
-    const float zw = depth_at(__int_as_float(q.q1.z), __int_as_float(q.q1.w), __int_as_float(q.q2.z), d.x, d.y);
-    const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
-    const uint64_t k = depth_key<NoDepth>(depth_q24(zc), (uint32_t)q.q2.w);
-    const bool win = in && zc == zw && k < best;
-    best = win ? k : best;
+    const float zw = depth_at(__int_as_float(q.q1.z), __int_as_float(q.q1.w), __int_as_float(q.q2.w), d.x, d.y);
+    if constexpr (NoDepth) {
+        // R4 range test without branches: in range iff the clamp leaves zw unchanged (false for NaN)
+        const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
+        const uint64_t k = depth_key<NoDepth>(depth_q24(zc), (uint32_t)q.q2.z);
+        const bool win = in && zc == zw && k < best;
+        best = win ? k : best;
+    } else {
+        // R4 with the far test folded into the key: zw >= 1 quantises to q >= 2^24-1 (v_cvt_u32 saturates),
+        // a key that never beats the initial one (cleared depth), so only zw >= 0 needs a test (false for
+        // NaN).  Inside [0, 1] q is depth_q24(zw): the same keys as the clamped form, one VALU less.
+        uint32_t qd;
+        asm("v_cvt_u32_f32 %0, %1" : "=v"(qd) : "v"(__builtin_fmaf(zw, 16777215.0f, 0.5f)));
+        const uint64_t k = ((uint64_t)qd << 32) | (uint32_t)q.q2.z;
+        const bool win = in && zw >= 0.0f && k < best;
+        best = win ? k : best;
+    }
 }
 
 __device__ __noinline__ bool covers_face_multi(int64_t hint_ri, const Rec *frame_recs, const FaceData *fdata_frame,
@@ -945,7 +993,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     int4 *d = reinterpret_cast<int4 *>(&t_ent[t]);
                     d[0] = make_int4(E.e[0], E.e[1], E.e[2], (int)E.ab[0]);
                     d[1] = make_int4((int)E.ab[1], (int)E.ab[2], __float_as_int(E.za), __float_as_int(E.zb));
-                    d[2] = make_int4(__float_as_int(E.fx0), __float_as_int(E.fy0), __float_as_int(E.z0), (int)E.key);
+                    d[2] = make_int4(__float_as_int(E.fx0), __float_as_int(E.fy0), (int)E.key, __float_as_int(E.z0));
                     m |= large ? 16u : 0u;
                 }
                 t_mask[t] = (uint8_t)m;
@@ -1976,8 +2024,12 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
     if (F > 0) {
         ProfScope ps(K_SETUP, stream);
-        launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream);
+        launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream, zero_grad_vertices,
+                        (int64_t)B * V * 4, zero_grad_vertex_colors, (int64_t)B * V * C);
         HIP_TRY(hipGetLastError());
+        // (the setup grid's filler workgroups zero the accumulators; the raster does it only when F == 0)
+        zero_grad_vertices = nullptr;
+        zero_grad_vertex_colors = nullptr;
     }
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
     ProfScope ps(K_RASTER, stream);
