@@ -836,6 +836,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      int sid, int tcb)
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
+#if defined(DIRT_RASTER_LDS_PAD) && DIRT_RASTER_LDS_PAD > 0
+    __shared__ volatile char occupancy_probe[DIRT_RASTER_LDS_PAD];  // experiment: caps workgroups per CU
+    if (threadIdx.x == 1023) occupancy_probe[0] = 0;
+#endif
     PHASE_TS(0);
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     const int C = CC > 0 ? CC : Cdyn;
@@ -1413,6 +1417,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     constexpr int NVM = 9 + 3 * CM;
     const int C = CC > 0 ? CC : Cdyn;
     const int NV = 9 + 3 * C;
+#if defined(DIRT_GRAD_LDS_PAD) && DIRT_GRAD_LDS_PAD > 0
+    __shared__ volatile char occupancy_probe[DIRT_GRAD_LDS_PAD];  // experiment: caps workgroups per CU
+    if (threadIdx.x == 1023) occupancy_probe[0] = 0;
+#endif
     __shared__ int32_t s_gb[kHaloPix];
     __shared__ uint8_t s_cov[kHaloPix];  // neighbour_coverage() bits of the pixel's face (forward)
     __shared__ int8_t s_slot[kHaloPix];  // slot of the pixel's record, -1 none, kNoSlot table full
