@@ -7,8 +7,8 @@ the C ABI, so a whole forward+backward step can be captured into a HIP graph (to
 replayed without host launch overhead.  Results are identical to the autograd path (same kernels).
 
 The session also removes the per-step housekeeping launches: the scratch is zero-filled once and every
-forward leaves it clean (DIRT_FWD_SCRATCH_CLEAN skips the forward's clearing memset), and the forward's
-raster kernel zero-fills the gradient accumulators in passing, so the backward adds into them
+forward leaves it clean (DIRT_FWD_SCRATCH_CLEAN skips the forward's clearing memset), and the forward
+zero-fills the gradient accumulators in passing (filler workgroups of its setup launch), so the backward adds into them
 (DIRT_BWD_ACCUMULATE) without a clearing kernel of its own.  Hence: the gradients returned by
 `backward` stay valid until the next `forward`, and each forward is followed by at most one backward.
 """

@@ -106,7 +106,7 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
  * B, H, W, F and bin_capacity is "clean". */
 #define DIRT_FWD_SCRATCH_CLEAN 1u /* the scratch is clean: skip the forward's own clearing memset */
 /* zero_grad_vertices [B,V,4] / zero_grad_vertex_colors [B,V,C] (each may be NULL): accumulators the
- * forward zero-fills in passing (inside its raster kernel), for a later dirt_rasterise_bwd with
+ * forward zero-fills in passing (filler workgroups of its setup launch, idle CUs), for a later dirt_rasterise_bwd with
  * DIRT_BWD_ACCUMULATE -- a fixed-shape training loop then pays no separate clearing launch.
  * Alignment: no pointer argument of this ABI needs more than its element's natural alignment (4 B);
  * 16-B aligned buffers (every torch / hipMalloc allocation) take the vectorised zero-fill path, others
