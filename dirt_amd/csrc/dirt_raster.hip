@@ -1514,11 +1514,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                 const uint32_t o = (uint32_t)((H - 1 - hj) * W + hi);
                 gbv[u] = gb_f[o];
                 cvv[u] = cov_f[o];
+                // one pixel's channels from one base address (o * C < 2^29): RGB becomes one
+                // global_load_dwordx3 per operand instead of three dword loads
+                const float *gq = gp_f + o * (uint32_t)C, *pq = px_f + o * (uint32_t)C;
 #pragma unroll
                 for (int c = 0; c < CM; ++c)
                     if (c < C) {
-                        Gv[u][c] = gp_f[o * C + c];
-                        Iv[u][c] = px_f[o * C + c];
+                        Gv[u][c] = gq[c];
+                        Iv[u][c] = pq[c];
                     }
             }
         }
@@ -1635,10 +1638,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     if (in_frame) {
         float *gbg_f = grad_bg + (int64_t)b * H * W * C;
         const uint32_t o = (uint32_t)((H - 1 - j) * W + i);
+        float *gbq = gbg_f + o * (uint32_t)C;  // (RGB: one global_store_dwordx3)
 #pragma unroll
         for (int c = 0; c < CM; ++c) {
             const float gv = s_G[kme * CP + c];
-            if (c < C) gbg_f[o * C + c] = rp < 0 ? gv : 0.0f;
+            if (c < C) gbq[c] = rp < 0 ? gv : 0.0f;
         }
     }
 
