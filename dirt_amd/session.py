@@ -21,7 +21,10 @@ class RasteriseSession:
     def __init__(self, B, H, W, C, V, F, device=None, bin_capacity=0, shader_id=_lib.SHADER_GOURAUD):
         self.dims = (B, H, W, C, V, F)
         self.shader_id = shader_id
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device(device) if device is not None else torch.device("cuda")
+        if dev.type == "cuda" and dev.index is None:  # "cuda" means the current device: compare as cuda:N
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         self.bin_capacity = int(bin_capacity)
         saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, self.bin_capacity)
         self.saved_bytes, self.scratch_bytes = saved_bytes, scratch_bytes

@@ -356,3 +356,69 @@ def test_forward_zero_fill_of_misaligned_accumulators():
     for a in (ga, gc):
         h = a.cpu().numpy()
         assert h[0] == 7.0 and h[-1] == 7.0 and np.all(h[1:-1] == 0.0)
+
+
+def _fwd_with_accumulators(t, B, H, W, C, V, F, fill=7.0):
+    """One dirt_rasterise_fwd that also zero-fills accumulators prefilled with `fill`; returns them."""
+    from dirt_amd import _lib
+    saved_b, scratch_b = _lib.workspace_sizes(B, H, W, C, V, F)
+    saved = torch.empty(saved_b, dtype=torch.uint8, device="cuda")
+    scratch = torch.zeros(scratch_b, dtype=torch.uint8, device="cuda")
+    px = torch.empty((B, H, W, C), device="cuda")
+    gb = torch.empty((B, H, W), dtype=torch.int32, device="cuda")
+    ga = torch.full((B, V, 4), fill, device="cuda")
+    gc = torch.full((B, V, C), fill, device="cuda")
+    lib = _lib.load()
+    _lib.check(lib.dirt_rasterise_fwd(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), None,
+                                      B, H, W, C, V, F, 0, px.data_ptr(), gb.data_ptr(), saved.data_ptr(), saved_b,
+                                      scratch.data_ptr(), scratch_b, 0, 0, ga.data_ptr(), gc.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    return px, ga, gc
+
+
+def test_forward_zero_fill_by_setup_filler_workgroups_batch():
+    # F > 0: the accumulators are zeroed by filler workgroups of the setup launch (grid rows of B frames,
+    # more than one filler block per row); pixels are unaffected by the extra workgroups
+    frames = [scenes.random_triangles(F=700, W=96, H=80, C=3, seed=20 + k) for k in range(3)]
+    host = [np.stack([fr[k] for fr in frames]) for k in range(4)]
+    t = [_gpu(a) for a in host]
+    B, H, W, C = host[0].shape
+    V, F = host[1].shape[1], host[3].shape[1]
+    px, ga, gc = _fwd_with_accumulators(t, B, H, W, C, V, F)
+    assert torch.count_nonzero(ga).item() == 0 and torch.count_nonzero(gc).item() == 0
+    ref_px, _, _ = oracle.rasterise_fwd(*host)
+    assert np.array_equal(px.cpu().numpy(), ref_px)
+
+
+def test_forward_zero_fill_without_faces():
+    # F == 0: no setup launch, the raster kernel zero-fills the accumulators itself
+    bg = np.random.default_rng(3).uniform(0, 1, (2, 24, 40, 3)).astype(np.float32)
+    v = np.zeros((2, 6, 4), np.float32)
+    c = np.zeros((2, 6, 3), np.float32)
+    f = np.zeros((2, 0, 3), np.int32)
+    t = [_gpu(a) for a in (bg, v, c, f)]
+    px, ga, gc = _fwd_with_accumulators(t, 2, 24, 40, 3, 6, 0)
+    assert torch.count_nonzero(ga).item() == 0 and torch.count_nonzero(gc).item() == 0
+    assert np.array_equal(px.cpu().numpy(), bg)
+
+
+def test_repeated_forwards_batch_of_large_frames_identical():
+    # eight 1024^2 frames: 2048 bin counters (spread over 256-B lines), zeroed each forward by the setup
+    # workgroups of the other parity; three forwards in a row through one session give identical outputs
+    from dirt_amd.session import RasteriseSession
+    frames = [scenes.random_triangles(F=3000, W=1024, H=1024, C=3, seed=40 + k) for k in range(8)]
+    host = [np.stack([fr[k] for fr in frames]) for k in range(4)]
+    t = [_gpu(a) for a in host]
+    B, H, W, C = host[0].shape
+    V, F = host[1].shape[1], host[3].shape[1]
+    sess = RasteriseSession(B, H, W, C, V, F, device="cuda")
+    outs = []
+    for _ in range(3):
+        sess.forward(*t)
+        torch.cuda.synchronize()
+        outs.append((sess.pixels.clone(), sess.gbuffer.clone()))
+    for px, gb in outs[1:]:
+        assert torch.equal(px, outs[0][0]) and torch.equal(gb, outs[0][1])
+    ref_px, ref_gb, _ = oracle.rasterise_fwd(host[0][:1], host[1][:1], host[2][:1], host[3][:1])
+    assert np.array_equal(outs[0][0][:1].cpu().numpy(), ref_px)
