@@ -26,7 +26,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 BWD_ACCUMULATE = 1     # dirt_rasterise_bwd flags

@@ -1996,7 +1996,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 5; }
+int dirt_abi_version(void) { return 6; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 

@@ -67,7 +67,8 @@ extern "C" {
                               test (last face wins), background = terrain lookup, uncovered pixels 0 */
 
 /* ABI version, bumped on any signature or workspace-layout change (4: + dirt_hill_fwd, shader ids 6 and 7;
- * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels) */
+ * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
+ * separate 256-B lines of the scratch) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
