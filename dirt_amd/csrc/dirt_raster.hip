@@ -599,6 +599,16 @@ inline TileGrid tile_grid(int ntx) { return TileGrid{ntx, (uint32_t)(((1ull << 3
 #ifndef DIRT_RASTER_LISTS
 #define DIRT_RASTER_LISTS 1  // per-wave entry lists (1) or the scalar bit-mask walk (0)
 #endif
+// Hierarchical depth culling (depth-tested programs): a wave whose list holds at least DIRT_RASTER_HZ_MIN
+// entries walks it in groups of 16 and skips every entry whose depth lower bound over the tile exceeds
+// the farthest depth its 64 pixels already hold -- such an entry can win no pixel.  Pays where depth
+// complexity is high (large overlapping triangles); short lists keep the plain loop.
+#ifndef DIRT_RASTER_HZ
+#define DIRT_RASTER_HZ 1
+#endif
+#ifndef DIRT_RASTER_HZ_MIN
+#define DIRT_RASTER_HZ_MIN 32
+#endif
 constexpr int kWaveList = 256 + 2;  // a staging round's entries + the even pad
 constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per wave and chunk (2 loads per lane in flight)
 // A staged record is "small" when every |A|, |B| < 2^15: its edge steps inside a strip are one
@@ -725,6 +735,39 @@ __device__ __forceinline__ int lane_rank(uint64_t mask)
 {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
+
+// maximum of v over the wave, wave-uniform: row_shr 1/2/4/8 leave each 16-lane row's maximum in its
+// last lane, four readlanes combine the rows (lanes shifted in from outside a row keep their own value)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false));
+    const uint32_t a = __builtin_amdgcn_readlane(v, 15), b = __builtin_amdgcn_readlane(v, 31);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 47), d = __builtin_amdgcn_readlane(v, 63);
+    return max(max(a, b), max(c, d));
+}
+
+#if DIRT_RASTER_HZ
+// Conservative lower bound of the quantised depth a staged small entry can reach in the wave's pixel
+// rectangle at (x0, y0): the plane's minimum over the rectangle is at the corner its slopes point away
+// from; every zw the raster computes is within 2^-23 (|za||dx| + |zb||dy| + |z0|) of the exact plane
+// (two roundings), so twice that margin, and two more quanta, keep the bound below every key the
+// entry can produce there.  NaN planes give 0 (never culled).
+__device__ __forceinline__ uint32_t entry_qmin(const StripEntry *ent, uint32_t off, int x0, int y0)
+{
+    lds_int4v *ve = (lds_int4v *)((const char *)ent + off);
+    const int4v q1 = ve[1], q2 = ve[2];
+    const float za = __int_as_float(q1.z), zb = __int_as_float(q1.w), z0 = __int_as_float(q2.w);
+    const float xa = (float)x0 + 0.5f - __int_as_float(q2.x), xb = (float)(x0 + kWaveW - 1) + 0.5f - __int_as_float(q2.x);
+    const float ya = (float)y0 + 0.5f - __int_as_float(q2.y), yb = (float)(y0 + kWaveH - 1) + 0.5f - __int_as_float(q2.y);
+    const float zc = depth_at(za, zb, z0, za > 0.0f ? xa : xb, zb > 0.0f ? ya : yb);
+    const float s = fabsf(za) * fmaxf(fabsf(xa), fabsf(xb)) + fabsf(zb) * fmaxf(fabsf(ya), fabsf(yb)) + fabsf(z0);
+    const float zq = __builtin_fmaf(__builtin_fmaf(-s, 0x1p-21f, zc), 16777215.0f, -2.0f);
+    return zq > 0.0f ? (uint32_t)fminf(zq, 16777215.0f) : 0u;
+}
+#endif
 
 template <bool NoDepth, bool Large>
 __device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__restrict__ frame_recs, short2v pix,
@@ -1038,18 +1081,43 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                         ns += __popcll(bs);
                         nl += __popcll(bl);
                     }
-                    if (lane == 0 && (ns & 1)) t_wl[wave][ns] = 256u * sizeof(StripEntry);
+                    if (lane == 0) t_wl[wave][ns] = 256u * sizeof(StripEntry);  // pad / sentinel
                     wave_lds_sync();
                     // two entries per iteration; the next pair's offsets are read before this pair is
                     // tested (reads at k + 2 <= ns + 1 stay inside the list)
                     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
                     typedef const volatile __attribute__((address_space(3))) u32x2 lds_u32x2;
-                    u32x2 oo = *(lds_u32x2 *)&t_wl[wave][0];
-                    for (int k = 0; k < ns; k += 2) {
-                        const EntryRegs qa = load_entry_at(t_ent, oo.x), qb = load_entry_at(t_ent, oo.y);
-                        oo = *(lds_u32x2 *)&t_wl[wave][k + 2];
-                        raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, i, j, best);
-                        raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, i, j, best);
+                    // Depth-tested programs with long lists (DIRT_RASTER_HZ): the list runs in segments -- the
+                    // first DIRT_RASTER_HZ_MIN entries as they are, then each following group of 64 compacted in
+                    // place (to its front) to the entries whose depth lower bound over the tile does not exceed
+                    // the farthest depth the wave's pixels hold; the others can win no pixel.  A segment starts
+                    // even (aligned pair reads); the second read of an odd segment's last pair lands on a
+                    // valid entry (stale or next) or the sentinel, and an entry run twice changes nothing (min).
+                    int base = 0;
+                    int seg = (!kNoDepth && DIRT_RASTER_HZ) ? min(ns, DIRT_RASTER_HZ_MIN) : ns;
+                    int rp = seg;  // first list position not yet run or culled
+                    for (;;) {
+                        u32x2 oo = *(lds_u32x2 *)&t_wl[wave][base];
+                        for (int k = base; k < base + seg; k += 2) {
+                            const EntryRegs qa = load_entry_at(t_ent, oo.x), qb = load_entry_at(t_ent, oo.y);
+                            oo = *(lds_u32x2 *)&t_wl[wave][k + 2];
+                            raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, i, j, best);
+                            raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, i, j, best);
+                        }
+                        if (kNoDepth || !DIRT_RASTER_HZ || rp >= ns) break;
+#if DIRT_RASTER_HZ
+                        const uint32_t wmax = wave_max_u32((uint32_t)(best >> 32));
+                        const int kk = rp + lane;
+                        const bool tst = kk < ns;
+                        const uint32_t off = tst ? t_wl[wave][kk] : 0u;
+                        const bool live = tst && entry_qmin(t_ent, off, ti0 + wave_ox(wave), tj0 + wave_oy(wave)) <= wmax;
+                        const uint64_t lm = __ballot(live);
+                        if (live) t_wl[wave][rp + lane_rank(lm)] = off;
+                        wave_lds_sync();
+                        base = rp;
+                        seg = __popcll(lm);
+                        rp = min(rp + 64, ns);
+#endif
                     }
                     for (int k = 0; k < nl; ++k)
                         raster_entry<kNoDepth, true>(load_entry(t_ent, (int)t_wl[wave][kWaveList - 1 - k]), frame_recs, pix,
@@ -1100,7 +1168,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             }
             // next chunk's slab entries (its filter runs after the next barrier-free LDS writes; t_list
             // is rewritten only after this chunk's last staging round)
-            if (!overflow && chunk + kStrips * kFilterBlock < n_items) load_chunk(chunk + kStrips * kFilterBlock);
+            if (!overflow && chunk + kStrips * kFilterBlock < n_items) {
+                load_chunk(chunk + kStrips * kFilterBlock);
+            } else {
+                // (no next chunk: defining ev on both paths ends its live range at the filter instead of
+                // keeping the stale entries in registers through the staging rounds)
+#pragma unroll
+                for (int u = 0; u < U; ++u) ev[u] = make_uint2(0u, 0u);
+            }
         }
     }
     PHASE_TS(3);

@@ -299,6 +299,24 @@ def test_large_triangle_stress_r64():
     check_scene(*scenes.random_triangles(F=4000, W=1024, H=1024, radius_px=64.0, seed=6))
 
 
+@pytest.mark.parametrize("perspective", [False, True])
+def test_deep_depth_complexity_culling(perspective):
+    """Hundreds of frame-sized triangles per 8x8 block: the raster's per-wave lists exceed
+    DIRT_RASTER_HZ_MIN, so most entries go through the depth-bound culling.  Exact ties (duplicate faces
+    on the same vertices: the lower face must win) and sub-quantum near-ties keep the bound honest."""
+    bg, v, c, f = scenes.random_triangles(F=400, W=96, H=80, radius_px=70.0, seed=11, perspective=perspective)
+    dup = f[:120].copy()                                   # identical planes, higher face index
+    near = f[120:200].copy()                               # own vertices, depth nudged by ~1e-7
+    vn = v[near.reshape(-1)].copy()
+    vn[:, 2] += np.float32(1e-7) * vn[:, 3]
+    near = (v.shape[0] + np.arange(near.size, dtype=np.int32)).reshape(-1, 3)
+    cn = c[f[120:200].reshape(-1)]
+    v2 = np.concatenate([v, vn]).astype(np.float32)
+    c2 = np.concatenate([c, cn]).astype(np.float32)
+    f2 = np.concatenate([f, dup, near]).astype(np.int32)
+    check_scene(bg, v2, c2, f2)
+
+
 def test_session_argument_checks():
     # camera_pos must be a device float32 tensor with the floats the program reads; a procedural
     # session has no gradient (ADVICE r1: the session checked less than the autograd path)

@@ -2,6 +2,7 @@
 through RasteriseSession replayed from HIP graphs (10 steps per graph), inputs resident in HBM.
 
     python tools/bench_configs.py > profiles/r01/configs.jsonl
+    python tools/bench_configs.py stress c5   # only the configs whose names contain these
 """
 import json
 import os
@@ -66,8 +67,11 @@ def run(name, frames, steps=100):
 
 
 def main():
+    # optional arguments: substrings selecting configs (all by default)
+    sel = sys.argv[1:]
     for name, make in CONFIGS.items():
-        print(json.dumps(run(name, make())), flush=True)
+        if not sel or any(k in name for k in sel):
+            print(json.dumps(run(name, make())), flush=True)
 
 
 if __name__ == "__main__":
