@@ -305,11 +305,13 @@ __device__ __forceinline__ void coarse_pairs_add(BigQueue &Q, int32_t ri, uint32
 }
 
 // Whole workgroup (converged): expand the queued records' pairs over all threads; resets the queue.
+// Returns the number of queued records; an empty queue costs one barrier.
 template <int NT, class Op>
-__device__ __forceinline__ void coarse_pairs_flush(BigQueue &Q, Op op)
+__device__ __forceinline__ int coarse_pairs_flush(BigQueue &Q, Op op)
 {
     __syncthreads();
     const int nq = min(Q.n, kBigCap);
+    if (nq == 0) return 0;  // (uniform; Q.n is already 0)
     if (threadIdx.x == 0) {
         Q.start[0] = 0;
         for (int q = 0; q < nq; ++q) Q.start[q + 1] += Q.start[q];
@@ -326,6 +328,7 @@ __device__ __forceinline__ void coarse_pairs_flush(BigQueue &Q, Op op)
     __syncthreads();
     if (threadIdx.x == 0) Q.n = 0;
     __syncthreads();
+    return nq;
 }
 
 // per-workgroup phase timestamps of the instrumented backward (AB & 128, dirt_debug_bwd_variant 128)
@@ -487,7 +490,8 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         fdata[gid] = fd;
     }
     PHASE_TS(1);
-    coarse_pairs_flush<kBinThreads>(Q, count);
+    // (the placement pass queues the same records again: with none queued here, it needs no flush)
+    const int nbig = coarse_pairs_flush<kBinThreads>(Q, count);
     PHASE_TS(2);
     // reserve this workgroup's range of every touched slab: one returning device atomic per (workgroup,
     // coarse tile), all in flight together
@@ -515,7 +519,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
             coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, place);
         }
     }
-    coarse_pairs_flush<kBinThreads>(Q, place);
+    if (nbig > 0) coarse_pairs_flush<kBinThreads>(Q, place);
     if (AB & 128) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
