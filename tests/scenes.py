@@ -227,3 +227,70 @@ def fullscreen_quad():
     v = np.array([[-1, -1, 0, 1], [-1, 1, 0, 1], [1, 1, 0, 1], [1, -1, 0, 1]], np.float32)
     f = np.array([[0, 1, 2], [0, 2, 3]], np.int32)
     return v, f
+
+
+def adversarial_scene(seed, W=64, H=48, C=3, F=300):
+    """Fuzz scene for the raster rules' edge cases, mixed at random: vertices snapped to pixel centres and
+    pixel edges (top-left rule ties), axis-aligned edges, fans sharing edges, slivers, sub-pixel
+    triangles, duplicated faces and coplanar overlaps (depth ties: the lower face wins), z beyond the
+    near / far planes, w near zero or negative (clipping), coordinates far outside the guard band."""
+    rng = np.random.default_rng(seed)
+    tris = []
+
+    def ndc_x(px):  # window x (pixels) -> NDC
+        return px * 2.0 / W - 1.0
+
+    def ndc_y(py):
+        return py * 2.0 / H - 1.0
+
+    for _ in range(F):
+        kind = rng.integers(0, 9)
+        z = rng.uniform(-0.9, 0.9)
+        if kind == 0:    # vertices on pixel centres
+            p = rng.integers(0, max(W, H), size=(3, 2)) + 0.5
+            t = [[ndc_x(a), ndc_y(b), z, 1.0] for a, b in p]
+        elif kind == 1:  # vertices on pixel corners, axis-aligned right triangle
+            x0, y0 = rng.integers(0, W), rng.integers(0, H)
+            s = rng.integers(1, 12)
+            t = [[ndc_x(x0), ndc_y(y0), z, 1.0], [ndc_x(x0 + s), ndc_y(y0), z, 1.0], [ndc_x(x0), ndc_y(y0 + s), z, 1.0]]
+        elif kind == 2:  # sliver: nearly collinear
+            a = rng.uniform(-1, 1, 2)
+            d = rng.uniform(-0.5, 0.5, 2)
+            n = np.array([-d[1], d[0]]) * rng.uniform(1e-4, 1e-2)
+            t = [[*a, z, 1.0], [*(a + d), z, 1.0], [*(a + 0.5 * d + n), z, 1.0]]
+        elif kind == 3:  # sub-pixel triangle
+            c = rng.uniform(-1, 1, 2)
+            o = rng.uniform(-0.8, 0.8, size=(3, 2)) * np.array([2.0 / W, 2.0 / H])
+            t = [[*(c + oo), z, 1.0] for oo in o]
+        elif kind == 4 and tris:  # duplicate of an earlier face (exact depth tie)
+            t = [list(vv) for vv in tris[rng.integers(0, len(tris))]]
+        elif kind == 5 and tris:  # coplanar overlap: an earlier face's plane, shifted in xy
+            base = np.array(tris[rng.integers(0, len(tris))], np.float64)
+            sh = rng.uniform(-0.05, 0.05, 2)
+            t = [[vv[0] + sh[0] * vv[3], vv[1] + sh[1] * vv[3], vv[2], vv[3]] for vv in base]
+        elif kind == 6:  # beyond near / far planes or straddling them
+            p = rng.uniform(-1, 1, size=(3, 2))
+            zz = rng.uniform(-1.6, 1.6, size=3)
+            t = [[p[k, 0], p[k, 1], zz[k], 1.0] for k in range(3)]
+        elif kind == 7:  # w near zero or negative (perspective clipping)
+            p = rng.uniform(-1, 1, size=(3, 2))
+            w = rng.choice([rng.uniform(-0.3, 0.3), rng.uniform(0.5, 2.0)], size=3)
+            t = [[p[k, 0] * abs(w[k]), p[k, 1] * abs(w[k]), z * abs(w[k]), w[k]] for k in range(3)]
+        else:            # fan sharing a centre vertex and edges with the previous fan triangle
+            c = rng.uniform(-0.8, 0.8, 2)
+            r = rng.uniform(0.02, 0.4)
+            a0 = rng.uniform(0, 2 * np.pi)
+            for k in range(3):
+                a1, a2 = a0 + k * 2.1, a0 + (k + 1) * 2.1
+                tris.append([[*c, z, 1.0], [c[0] + r * np.cos(a1), c[1] + r * np.sin(a1), z, 1.0],
+                             [c[0] + r * np.cos(a2), c[1] + r * np.sin(a2), z, 1.0]])
+            continue
+        tris.append(t)
+    if rng.uniform() < 0.5:  # one triangle far outside the guard band
+        tris.append([[-4000.0, -3000.0, 0.3, 1.0], [5000.0, -2000.0, 0.3, 1.0], [100.0, 6000.0, 0.3, 1.0]])
+    v = np.array(tris, np.float64).reshape(-1, 4).astype(np.float32)
+    nf = len(tris)
+    faces = np.arange(3 * nf, dtype=np.int32).reshape(nf, 3)
+    cols = rng.uniform(0, 1, size=(3 * nf, C)).astype(np.float32)
+    bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
+    return bg, v, cols, faces

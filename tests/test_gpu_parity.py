@@ -317,6 +317,25 @@ def test_deep_depth_complexity_culling(perspective):
     check_scene(bg, v2, c2, f2)
 
 
+@pytest.mark.parametrize("seed", range(36))
+def test_fuzz_adversarial_scenes(seed):
+    """Raster-rule edge cases mixed at random (scenes.adversarial_scene): pixel-centre / pixel-edge
+    vertices, slivers, sub-pixel triangles, duplicate and coplanar faces, near / far / w <= 0 clipping,
+    guard-band overflow; three frame shapes, one batch of two."""
+    W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
+    if seed % 4 == 3:
+        frames = [scenes.adversarial_scene(seed * 10 + k, W=W, H=H, F=150) for k in range(2)]
+        F = max(fr[3].shape[0] for fr in frames)
+        # pad the shorter frame with degenerate faces so both frames share F
+        frames = [(bg, v, c, np.concatenate([f, np.zeros((F - f.shape[0], 3), np.int32)])) for bg, v, c, f in frames]
+        V = max(fr[1].shape[0] for fr in frames)
+        frames = [(bg, np.concatenate([v, np.tile(v[:1], (V - v.shape[0], 1))]),
+                   np.concatenate([c, np.tile(c[:1], (V - c.shape[0], 1))]), f) for bg, v, c, f in frames]
+        check_scene(*[np.stack([fr[k] for fr in frames]) for k in range(4)], seed=seed)
+    else:
+        check_scene(*scenes.adversarial_scene(seed, W=W, H=H), seed=seed)
+
+
 def test_session_argument_checks():
     # camera_pos must be a device float32 tensor with the floats the program reads; a procedural
     # session has no gradient (ADVICE r1: the session checked less than the autograd path)
