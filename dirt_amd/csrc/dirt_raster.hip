@@ -668,6 +668,26 @@ __device__ __forceinline__ void depth_update(const Rec &r, uint32_t key, float f
     best = win ? k : best;
 }
 
+// stage_tile's block mask of a large record (some |A|, |B| >= 2^15) in int64, out of line (rare)
+__device__ __noinline__ uint32_t large_block_mask(const Rec *rp, int32_t px0, int32_t py0, uint32_t mask)
+{
+    const RasterPart R = *reinterpret_cast<const RasterPart *>(rp);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
+        const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
+        const int64_t a = (int64_t)R.A[k] * 256, bb = (int64_t)R.B[k] * 256;
+        // over a wave's rectangle [ox, ox + kWaveW) x [oy, oy + kWaveH): max of E at its origin + the
+        // positive parts of the steps across it
+        const int64_t wx = a * (kWaveW - 1), wy = bb * (kWaveH - 1);
+        const int64_t wmax = (wx > 0 ? wx : 0) + (wy > 0 ? wy : 0);
+#pragma unroll
+        for (int st = 0; st < kStrips; ++st)
+            if (e0 + a * wave_ox(st) + bb * wave_oy(st) + wmax <= 0) mask &= ~(1u << st);
+    }
+    return mask;
+}
+
 // Stage one tile survivor (record ri) for the 16x16 tile at pixel (ti0, tj0): edge values at the tile
 // origin (E + owned, exact int32, pinned to 2^30 where the edge holds over the whole tile), the packed
 // (A, B) steps, depth plane and key.  Returns the mask of the tile's four wave rectangles (8x8 blocks) the
@@ -689,22 +709,28 @@ __device__ __forceinline__ uint32_t stage_tile(const Rec *__restrict__ frame_rec
             mask |= 1u << st;
     }
     const int32_t px0 = ti0 * 256 + 128, py0 = tj0 * 256 + 128;
+    // E at the tile origin in int64, clamped to +-2^30; for a small record (|A|, |B| < 2^15: steps
+    // across the tile < 2^23) that keeps every block decision and the pinning exact, so the rest is
+    // int32.  A large record's block mask is redone in int64 out of line (rare).
+    const uint32_t bbox_mask = mask;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
-        const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
-        const int64_t a = (int64_t)R.A[k] * 256, bb = (int64_t)R.B[k] * 256;
-        // over a wave's rectangle [ox, ox + kWaveW) x [oy, oy + kWaveH): max of E at its origin + the
-        // positive parts of the steps across it
-        const int64_t wx = a * (kWaveW - 1), wy = bb * (kWaveH - 1);
-        const int64_t wmax = (wx > 0 ? wx : 0) + (wy > 0 ? wy : 0);
+        const int32_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
+        const int64_t e64 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
+        const int32_t e0 = e64 > (1 << 30) ? (1 << 30) : e64 < -(1 << 30) ? -(1 << 30) : (int32_t)e64;
+        // (wrapping uint32 arithmetic: a large record's values may wrap here -- its mask is redone below
+        // and its edge values are unused -- a small record's never do)
+        const uint32_t a = (uint32_t)R.A[k] << 8, bb = (uint32_t)R.B[k] << 8;
+        const int32_t wx = (int32_t)(a * (kWaveW - 1)), wy = (int32_t)(bb * (kWaveH - 1));
+        const uint32_t wmax = (uint32_t)(wx > 0 ? wx : 0) + (uint32_t)(wy > 0 ? wy : 0);
 #pragma unroll
         for (int st = 0; st < kStrips; ++st)
-            if (e0 + a * wave_ox(st) + bb * wave_oy(st) + wmax <= 0) mask &= ~(1u << st);
-        const int64_t tx = a * (kTile - 1), ty = bb * (kTile - 1);
-        E.e[k] = e0 + (tx < 0 ? tx : 0) + (ty < 0 ? ty : 0) > 0 ? (1 << 30) : (int32_t)e0;
+            if ((int32_t)((uint32_t)e0 + a * wave_ox(st) + bb * wave_oy(st) + wmax) <= 0) mask &= ~(1u << st);
+        const int32_t tx = (int32_t)(a * (kTile - 1)), ty = (int32_t)(bb * (kTile - 1));
+        E.e[k] = (int32_t)((uint32_t)e0 + (uint32_t)(tx < 0 ? tx : 0) + (uint32_t)(ty < 0 ? ty : 0)) > 0 ? (1 << 30) : e0;
         E.ab[k] = ((uint32_t)R.A[k] & 0xffffu) | ((uint32_t)R.B[k] << 16);
     }
+    if (__builtin_amdgcn_ballot_w64(!small) != 0 && !small) mask = large_block_mask(&frame_recs[ri], px0, py0, bbox_mask);
     if (!small) {
         E.e[0] = ri;
         E.ab[0] = kLargeAB;
