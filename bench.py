@@ -103,8 +103,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
-    ap.add_argument("--graph-steps", type=int, default=10,
-                    help="steps captured per HIP graph (each replay runs that many complete steps)")
+    ap.add_argument("--graph-steps", type=int, default=200,
+                    help="steps captured per HIP graph (each replay runs that many complete steps; default: all "
+                         "timed steps up to 200 in one graph, since every replay boundary costs ~24 us)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--profile-steps", type=int, default=50)
