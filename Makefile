@@ -20,7 +20,7 @@ ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wa
 LIB = dirt_amd/libdirt_mi355x.so
 ORACLE = oracle/libdirt_oracle.so
 HIP_SRC = dirt_amd/csrc/dirt_raster.hip
-HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h
+HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/setup_kernel.h dirt_amd/csrc/raster_kernel.h dirt_amd/csrc/grad_kernel.h dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h
 
 all: $(LIB) $(ORACLE)
 

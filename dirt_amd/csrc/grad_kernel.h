@@ -1,0 +1,745 @@
+// Part of dirt_raster.hip's translation unit: included inside its anonymous namespace after the shared
+// definitions (raster_rules.h, oceanic.h, hill.h, the layout and error helpers).  Not a standalone header.
+
+// ------------------------------------------------------------------------------------------------
+// K5: backward
+//
+// One 256-thread workgroup per 16x16 tile, one lane per pixel.  Every contribution of a lane goes to
+// the face visible at its own pixel: colour gradients lambda_k * G, and the share of the four
+// neighbour pairs around the pixel that this face owns (a pair's other owner is handled by the lane
+// on the other side, same-face pairs by the lower lane only).  Reduction without global contention:
+//   1. DPP segmented scan along each 16-pixel row (one DPP row == one pixel row) sums runs of equal
+//      record index into the run's last lane;
+//   2. run tails write their partial sums into their record's contiguous LDS range (records kept in a
+//      per-tile LDS hash table keyed by record index, vertex ids cached);
+//   3. one wave-instruction of global float atomics per (tile, record): <= 9+3C lanes, ~3 cache lines.
+
+// Does face f cover pixel (i,j)?  `hint` is the record of f covering a neighbouring pixel; the other
+// sub-records of f are only consulted when f was clipped into several (`multi`).
+__device__ __forceinline__ bool edge_covers(const EdgePart &r, int i, int j)
+{
+    // empty records have i0 > i1 and are rejected by the bbox test
+    if (r.i0 > r.i1 || i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1) return false;
+    int64_t E[3];
+    edge_values(r, i, j, E);
+    return inside(r, E);
+}
+
+__device__ __noinline__ bool covers_face_multi(int64_t hint_ri, const Rec *frame_recs, const FaceData *fdata_frame,
+                                               int F, int f, int i, int j)
+{
+    const int n = fdata_frame[f].nsub;
+    for (int s = 0; s < n; ++s) {
+        const int64_t ri = rec_index(F, f, s);
+        if (ri == hint_ri) continue;
+        if (edge_covers(*reinterpret_cast<const EdgePart *>(&frame_recs[ri]), i, j)) return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool covers_face(const EdgePart &hint, int64_t hint_ri, bool multi, const Rec *frame_recs,
+                            const FaceData *fdata_frame, int F, int f, int i, int j)
+{
+    if (edge_covers(hint, i, j)) return true;
+    if (!multi) return false;
+    return covers_face_multi(hint_ri, frame_recs, fdata_frame, F, f, i, j);
+}
+
+template <int D>
+__device__ __forceinline__ float dpp_shr_f(float v)  // lane l <- lane l-D of the same 16-lane row, 0 if none
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x110 + D, 0xF, 0xF, true));
+}
+template <int D>
+__device__ __forceinline__ int dpp_shr_i(int v, int fill)
+{
+    return __builtin_amdgcn_update_dpp(fill, v, 0x110 + D, 0xF, 0xF, false);
+}
+template <int D>
+__device__ __forceinline__ int dpp_shl_i(int v, int fill)  // lane l <- lane l+D of the same row
+{
+    return __builtin_amdgcn_update_dpp(fill, v, 0x100 + D, 0xF, 0xF, false);
+}
+
+// int64 -> f32 with two conversions (may double-round: backward-only, tolerance-level)
+__device__ __forceinline__ float fast_i64_to_f32(int64_t v)
+{
+    const int32_t hi = (int32_t)(v >> 32);
+    const uint32_t lo = (uint32_t)v;
+    return fmaf((float)hi, 4294967296.0f, (float)lo);
+}
+
+// perspective-correct barycentrics from a_k = E_k / w_k (R6) with one fast reciprocal
+__device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, float a1, float a2, float lam[3])
+{
+    const float s = (a0 + a1) + a2;
+    if (s == 0.0f) return false;
+    const float rs = __builtin_amdgcn_rcpf(s);
+    const float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
+    if (!multi) {
+        lam[0] = m0; lam[1] = m1; lam[2] = m2;
+        return true;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
+    return true;
+}
+
+#ifndef DIRT_GRAD_WAVES
+#define DIRT_GRAD_WAVES 6  // min waves per SIMD the register allocation must allow
+#endif
+#ifndef DIRT_GRAD_WAVES_C3
+#define DIRT_GRAD_WAVES_C3 8  // C = 3: 64 VGPRs without spills (then 7 workgroups per CU, LDS-bound);
+                              // C = 1 spills at 8, the generic paths are LDS-bound at 5
+#endif
+#ifndef DIRT_GRAD_ATTR
+#define DIRT_GRAD_ATTR
+#endif
+
+// window-transform constants of the chain rule, computed on the host (IEEE, as the oracle)
+struct NdcScale {
+    float inv_hw, inv_hh, half_w, half_h;
+};
+
+constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
+constexpr int kHaloPix = kHalo * kHalo;
+constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS (typ. 10-40)
+constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
+static_assert(kSlots <= 128, "slot ids (0 .. kSlots-1) are stored as int8");
+
+// LDS-resident copy of the edge part of the records seen in a tile + halo (for coverage tests of a
+// neighbour's face) and of their vertex ids (for the flush).
+struct SlotTable {
+    int32_t key[kSlots];     // g-buffer word (record index | clipped flag), -1 = free
+    int8_t list[kSlots];     // occupied slots in insertion order
+    int32_t A[3][kSlots], B[3][kSlots];
+    int32_t e[3][kSlots];      // small records: E + owned at the halo origin pixel (see kGradSmallEdge)
+    uint32_t bx[kSlots], by[kSlots];  // i0 | i1 << 16 (bit 31: large record, use the global Rec)
+    int32_t v[3][kSlots];    // vertex ids, indexed by list position
+    float iw[3][kSlots], w[3][kSlots];  // interpolation data of the record (own-pixel path)
+    float h2d[kSlots];                  // 1 / (2 D), D = E0 + E1 + E2 (constant over the plane)
+    int32_t n;
+};
+
+// A record is "small" for the backward when every |A|, |B| < 2^14 (edges shorter than 64 px).  Such a
+// record is visible somewhere in the 18x18 tile + halo region, so at every region pixel its edge values
+// satisfy |E| < 2^28 (E at a covered pixel) + 2 * 2^14 * 17 * 256 < 2^30: exact in int32, and a
+// coverage test is E0 + A*256*hx + B*256*hy with 24-bit multiplies (hx, hy in 0..17).
+constexpr int32_t kGradSmallEdge = 1 << 14;
+constexpr uint32_t kSlotLarge = 0x80000000u;
+
+__device__ __forceinline__ bool slot_is_large(const SlotTable &T, int s) { return (T.bx[s] & kSlotLarge) != 0; }
+
+// exact coverage of region pixel (hx, hy) = absolute (i, j) by small slot s (bbox + R2/R3 edge test)
+__device__ __forceinline__ bool slot_covers_small(const SlotTable &T, int s, int hx, int hy, int i, int j)
+{
+    const uint32_t bx = T.bx[s], by = T.by[s];
+    if (i < (int)(bx & 0xffff) || i > (int)((bx >> 16) & 0x7fff) || j < (int)(by & 0xffff) || j > (int)(by >> 16))
+        return false;
+    const int32_t x = hx * 256, y = hy * 256;
+    const int32_t e0 = T.e[0][s] + __mul24(T.A[0][s], x) + __mul24(T.B[0][s], y);
+    const int32_t e1 = T.e[1][s] + __mul24(T.A[1][s], x) + __mul24(T.B[1][s], y);
+    const int32_t e2 = T.e[2][s] + __mul24(T.A[2][s], x) + __mul24(T.B[2][s], y);
+    return min(e0, min(e1, e2)) > 0;
+}
+
+__device__ __forceinline__ int32_t owned_bit(int32_t A, int32_t B) { return (A > 0 || (A == 0 && B < 0)) ? 1 : 0; }
+
+__device__ __forceinline__ int slot_hash(int32_t key) { return (int)(((uint32_t)key * 2654435761u) >> 25) & (kSlots - 1); }
+
+// Insert `key` for every lane with `want` (called by the whole wave, converged): probes advance in
+// lockstep, and the lanes that created a slot append it to the slot list with one atomic per wave.
+// Returns the slot, kNoSlot if the table is full, -1 where !want.
+__device__ __forceinline__ int slot_insert_wave(SlotTable &T, int32_t key, bool want)
+{
+    int slot = slot_hash(key);
+    int result = want ? kNoSlot : -1;
+    bool pending = want, fresh = false;
+    for (int probe = 0; probe < kSlots; ++probe) {
+        if (!__any(pending)) break;
+        if (pending) {
+            const int old = atomicCAS(&T.key[slot], -1, key);
+            if (old == -1 || old == key) {
+                result = slot;
+                fresh = old == -1;
+                pending = false;
+            } else {
+                slot = (slot + 1) & (kSlots - 1);
+            }
+        }
+    }
+    const uint64_t mask = __ballot(fresh);
+    if (mask) {
+        int base = 0;
+        if ((threadIdx.x & 63) == 0) base = atomicAdd(&T.n, __popcll(mask));
+        base = __shfl(base, 0, 64);
+        if (fresh)
+            T.list[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = (int8_t)result;
+    }
+    return result;
+}
+
+// pair scalar s = -0.5 sum_c (G(p)+G(q)) (I(q)-I(p)) of staged pixels p = k, q = k2 (same operand order
+// as the oracle), 0 when either is outside the frame; every operand read unconditionally (no branches
+// between the LDS reads)
+template <int CP, int CM>
+__device__ __forceinline__ float pair_scalar(const int32_t *s_gb, const float *s_G, const float *s_I, int k, int k2, int C)
+{
+    const int32_t g1 = s_gb[k], g2 = s_gb[k2];
+    float a = 0.0f;
+    if (CP == 4 && CM == 3) {
+        typedef float f3v __attribute__((ext_vector_type(3)));  // ds_read_b96: 3 registers per operand
+        const f3v Gp = *reinterpret_cast<const f3v *>(&s_G[k * 4]), Gq = *reinterpret_cast<const f3v *>(&s_G[k2 * 4]);
+        const f3v Ip = *reinterpret_cast<const f3v *>(&s_I[k * 4]), Iq = *reinterpret_cast<const f3v *>(&s_I[k2 * 4]);
+        a = (Gp.x + Gq.x) * (Iq.x - Ip.x);
+        a = a + (Gp.y + Gq.y) * (Iq.y - Ip.y);
+        a = a + (Gp.z + Gq.z) * (Iq.z - Ip.z);
+    } else {
+        for (int c = 0; c < C; ++c) a += (s_G[k * CP + c] + s_G[k2 * CP + c]) * (s_I[k2 * CP + c] - s_I[k * CP + c]);
+    }
+    return (g1 != -2 && g2 != -2) ? -0.5f * a : 0.0f;
+}
+
+// Index (0..15) of the first lane of this lane's run of equal `key` in its 16-lane DPP row.
+__device__ __forceinline__ int run_start(int key, int lx)
+{
+    const int kl = dpp_shr_i<1>(key, -3);
+    int start = (lx == 0 || kl != key) ? lx : -1;
+    start = max(start, dpp_shr_i<1>(start, -1));
+    start = max(start, dpp_shr_i<2>(start, -1));
+    start = max(start, dpp_shr_i<4>(start, -1));
+    start = max(start, dpp_shr_i<8>(start, -1));
+    return start;
+}
+
+// AB: ablation mask for tools/ablate.py (0 in the product): 1 skip pairs, 2 skip colour weights,
+// 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
+// 32 skip the DPP run scan (every lane adds into LDS), 128 phase timestamps, 256 flush sums without
+// the global atomics
+template <int CC, int AB = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
+                          amdgpu_waves_per_eu(CC == 3 ? DIRT_GRAD_WAVES_C3 : DIRT_GRAD_WAVES))) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+                                                   const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
+                                                   const Rec *__restrict__ recs,
+                                                   const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
+                                                   int V, int F, TileGrid tg, int64_t nrec, float *__restrict__ grad_verts,
+                                                   float *__restrict__ grad_colors, float *__restrict__ grad_bg,
+                                                   const NdcScale ns)
+{
+    constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
+    constexpr int CP = CM == 3 ? 4 : CM;  // LDS pixel stride (float4 for RGB)
+    constexpr int NVM = 9 + 3 * CM;
+    const int C = CC > 0 ? CC : Cdyn;
+    const int NV = 9 + 3 * C;
+#if defined(DIRT_GRAD_LDS_PAD) && DIRT_GRAD_LDS_PAD > 0
+    __shared__ volatile char occupancy_probe[DIRT_GRAD_LDS_PAD];  // experiment: caps workgroups per CU
+    if (threadIdx.x == 1023) occupancy_probe[0] = 0;
+#endif
+    __shared__ int32_t s_gb[kHaloPix];
+    __shared__ uint8_t s_cov[kHaloPix];  // neighbour_coverage() bits of the pixel's face (forward)
+    __shared__ int8_t s_slot[kHaloPix];  // slot of the pixel's record, -1 none, kNoSlot table full
+#ifndef DIRT_GRAD_PAIR_RECOMPUTE
+#define DIRT_GRAD_PAIR_RECOMPUTE 1
+#endif
+    // RGB: each lane recomputes the pair scalars of its four pairs in phase B instead of staging them
+    // (LDS 22 -> 19 KiB: 8 workgroups per CU instead of 7); other channel counts stage them in phase A
+    constexpr bool kRecompute = DIRT_GRAD_PAIR_RECOMPUTE && CM == 3;
+    __shared__ float s_sx[kRecompute ? 1 : kHaloPix];  // pair scalar s of (k, k+x) and (k, k+y), DESIGN.md 4
+    __shared__ float s_sy[kRecompute ? 1 : kHaloPix];
+    // G / I of the staged pixels (phases A-B), then reused for the run-tail partial sums (C-D):
+    // keeps the workgroup at ~26 KB of LDS (6 per CU)
+    constexpr int kUnion = 2 * kHaloPix * CP;
+    constexpr int kTailCap = kUnion / NVM;
+    __shared__ __attribute__((aligned(16))) float s_u[kUnion];
+    float *const s_G = s_u;
+    float *const s_I = s_u + kHaloPix * CP;
+    float *const s_part = s_u;
+    // pair scalar of the pair (klo, klo + x) (axis 0) or (klo, klo + kHalo) (axis 1)
+    auto pair_s = [&](int axis, int klo) -> float {
+        if constexpr (kRecompute)
+            return pair_scalar<CP, CM>(s_gb, s_G, s_I, klo, klo + (axis == 0 ? 1 : kHalo), C);
+        else
+            return axis == 0 ? s_sx[klo] : s_sy[klo];
+    };
+    __shared__ SlotTable T;
+    // per slot: its number of row runs (= run tails), then the start (a cursor during the tail phase)
+    // of its contiguous range of tail partials in s_part
+    __shared__ int32_t s_tcnt[kSlots];
+    __shared__ int32_t s_toff[kSlots];
+    __shared__ int32_t s_lbeg[kSlots], s_lcnt[kSlots];  // the same ranges by list position (flush)
+
+    const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
+    int tx, ty;
+    tg.split(tile, tx, ty);
+    const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
+    const int i = tx * kTile + lx, j = ty * kTile + ly;
+    const Rec *frame_recs = recs + (int64_t)b * nrec;
+    const FaceData *fdata_frame = fdata + (int64_t)b * F;
+    // uniform: readfirstlane (convergent) keeps the divisions at the top instead of in every pair branch
+    const float inv_hw = ns.inv_hw, inv_hh = ns.inv_hh;  // 2/W, 2/H from the host (no division in the kernel)
+    const int kme = (ly + 1) * kHalo + (lx + 1);
+    const bool in_frame = i < W && j < H;
+
+    // ---- phase A: stage g-buffer / G / I of the tile + one-pixel halo, pair scalars, slot table
+    PHASE_TS(0);
+    for (int k = t; k < kSlots; k += 256) {
+        T.key[k] = -1;
+        s_tcnt[k] = 0;
+    }
+    if (t == 0) T.n = 0;
+    const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
+    {
+        // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * 256)
+        static_assert(kHaloPix <= 512, "two staging passes");
+        // frame base pointers (64-bit, uniform) + 32-bit per-lane offsets: H * W * C < 2^29
+        const int64_t fpix = (int64_t)b * H * W;
+        const int32_t *gb_f = gbuffer + fpix;
+        const uint8_t *cov_f = covbits + fpix;
+        const float *gp_f = grad_pixels + fpix * C, *px_f = pixels + fpix * C;
+        int32_t gbv[2];
+        uint32_t cvv[2];
+        float Gv[2][CM], Iv[2][CM];
+        bool ok[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = t + 256 * u;
+            const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
+            ok[u] = k < kHaloPix && hi >= 0 && hj >= 0 && hi < W && hj < H;
+            gbv[u] = -2;
+            cvv[u] = 0;
+            if (ok[u]) {
+                const uint32_t o = (uint32_t)((H - 1 - hj) * W + hi);
+                gbv[u] = gb_f[o];
+                cvv[u] = cov_f[o];
+                // one pixel's channels from one base address (o * C < 2^29): RGB becomes one
+                // global_load_dwordx3 per operand instead of three dword loads
+                const float *gq = gp_f + o * (uint32_t)C, *pq = px_f + o * (uint32_t)C;
+#pragma unroll
+                for (int c = 0; c < CM; ++c)
+                    if (c < C) {
+                        Gv[u][c] = gq[c];
+                        Iv[u][c] = pq[c];
+                    }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = t + 256 * u;
+            if (k >= kHaloPix) continue;
+            s_gb[k] = gbv[u];
+            s_cov[k] = (uint8_t)cvv[u];
+            if (!ok[u]) continue;
+            if constexpr (CM == 3) {
+                *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(Gv[u][0], Gv[u][1], Gv[u][2], 0.0f);
+                *reinterpret_cast<float4 *>(&s_I[k * CP]) = make_float4(Iv[u][0], Iv[u][1], Iv[u][2], 0.0f);
+            } else {
+#pragma unroll
+                for (int c = 0; c < CM; ++c)
+                    if (c < C) {
+                        s_G[k * CP + c] = Gv[u][c];
+                        s_I[k * CP + c] = Iv[u][c];
+                    }
+            }
+        }
+    }
+    __syncthreads();
+    PHASE_TS(1);
+    const int32_t gp = in_frame ? s_gb[kme] : -2;
+    {
+        const int rt = (t & 63) * 4 + (t >> 6);  // 0..255 spread over the four waves
+        // the tile's own records (run heads only; all distinct keys may not fit: the rest read global
+        // memory).  The halo's records are not needed: pair coverage comes from the forward's bits.
+        (void)rt;
+        const int32_t g = s_gb[kme];
+        const int key = g >= 0 ? g : -1;
+        const int start = run_start(key, lx);
+        int slot = slot_insert_wave(T, key, key >= 0 && start == lx);
+        if (key >= 0 && start == lx && slot >= 0) atomicAdd(&s_tcnt[slot], 1);  // one run (one tail later)
+        slot = __shfl(slot, (t & 48) + start, 64);
+        s_slot[kme] = key >= 0 ? slot : -1;
+    }
+    __syncthreads();
+    PHASE_TS(2);
+    PHASE_TS(3);
+    const int nslots = T.n;
+    static_assert(kSlots <= 64, "one slot per lane of wave 0");
+    if (t < 64) {
+        // wave 0: each slot's range of run-tail partials, in slot-list order (exclusive prefix)
+        const int sl = t < nslots ? T.list[t] : 0;
+        const int cnt = t < nslots ? s_tcnt[sl] : 0;
+        int inc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(inc, d, 64);
+            inc += t >= d ? v : 0;
+        }
+        if (t < nslots) {
+            s_toff[sl] = inc - cnt;
+            s_lbeg[t] = inc - cnt;
+            s_lcnt[t] = cnt;
+        }
+    }
+    {
+        // slot fill: the record loads are issued first and land while the pair scalars are computed
+        const bool filler = t < nslots;
+        int sf = 0;
+        EdgePart ep{};
+        FaceData fd{};
+        float riw0 = 0.f, riw1 = 0.f, riw2 = 0.f;
+        if (filler) {
+            sf = T.list[t];
+            const int32_t ri = T.key[sf] & kGbufIndexMask;
+            ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
+            fd = fdata_frame[face_of_record(ri, F)];
+            const Rec &r = frame_recs[ri];
+            riw0 = r.iw[0]; riw1 = r.iw[1]; riw2 = r.iw[2];
+        }
+        // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
+        // bottom row of the halo (their one pair into the tile); nothing reads the others
+        if constexpr (!kRecompute) {
+        const int rt = (t & 63) * 4 + (t >> 6);
+        s_sx[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + 1, C);
+        s_sy[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + kHalo, C);
+        if (rt < 16) {
+            const int k = (rt + 1) * kHalo;  // (0, rt + 1)
+            s_sx[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + 1, C);
+        } else if (rt < 32) {
+            const int k = rt - 15;  // (rt - 15, 0)
+            s_sy[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + kHalo, C);
+        }
+        }
+        if (filler) {
+            bool small = true;
+            int64_t E0[3];
+            edge_values(ep, hi0, hj0, E0);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                T.A[k][sf] = ep.A[k]; T.B[k][sf] = ep.B[k];
+                T.v[k][t] = fd.v[k];  // by list position (read only by the flush)
+                T.w[k][sf] = fd.w[k];
+                small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
+                        ep.B[k] < kGradSmallEdge;
+                T.e[k][sf] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
+            }
+            T.iw[0][sf] = riw0; T.iw[1][sf] = riw1; T.iw[2][sf] = riw2;
+            T.h2d[sf] = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
+            T.bx[sf] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
+            T.by[sf] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
+        }
+    }
+    __syncthreads();
+    PHASE_TS(4);
+
+    // ---- phase B: per-pixel contributions to the face visible at this pixel
+    const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
+    if (in_frame) {
+        float *gbg_f = grad_bg + (int64_t)b * H * W * C;
+        const uint32_t o = (uint32_t)((H - 1 - j) * W + i);
+        float *gbq = gbg_f + o * (uint32_t)C;  // (RGB: one global_store_dwordx3)
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+            const float gv = s_G[kme * CP + c];
+            if (c < C) gbq[c] = rp < 0 ? gv : 0.0f;
+        }
+    }
+
+    float acc[NVM];
+#pragma unroll
+    for (int v = 0; v < NVM; ++v) acc[v] = 0.0f;
+    const int sp = rp >= 0 ? s_slot[kme] : -1;
+    if (rp >= 0) {
+        // Ownership decisions (coverage tests) are exact int64; the interpolation weights use fast
+        // reciprocals (contributions agree with the oracle to ~1e-6 relative, far inside the 1e-4
+        // tolerance the atomic summation order already needs).  The own record comes through the
+        // vector-memory path (L1-resident: a wave touches a handful of records).
+        const int f = face_of_record(rp, F);
+        const bool multi = (gp & kGbufMulti) != 0;
+        // the own record (large records and the basis of clipped faces): its address is recomputed at
+        // each use from rp (the asm hides the common subexpression) instead of living in two registers
+        auto rec = [&]() -> const Rec & {
+            int r2 = rp;
+            asm volatile("" : "+v"(r2));
+            return frame_recs[r2];
+        };
+        const int hx = lx + 1, hy = ly + 1;  // region coordinates of this pixel
+        int32_t mA[3], mB[3], eme[3];       // eme: E + owned here (small records only)
+        float iw0, iw1, iw2, h2d;
+        float fEp[3];
+        bool me_small;
+        if (sp >= 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { mA[k] = T.A[k][sp]; mB[k] = T.B[k][sp]; }
+            iw0 = T.iw[0][sp]; iw1 = T.iw[1][sp]; iw2 = T.iw[2][sp];
+            h2d = T.h2d[sp];
+            me_small = !slot_is_large(T, sp);
+        } else {
+            const Rec &rr = rec();
+            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { mA[k] = me.A[k]; mB[k] = me.B[k]; }
+            iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
+            int64_t E0[3];
+            edge_values(me, i, j, E0);
+            h2d = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
+            me_small = false;
+        }
+        if (me_small) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                eme[k] = T.e[k][sp] + __mul24(mA[k], hx * 256) + __mul24(mB[k], hy * 256);
+                fEp[k] = (float)(eme[k] - owned_bit(mA[k], mB[k]));
+            }
+        } else {
+            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rec());
+            int64_t Ep[3];
+            edge_values(me, i, j, Ep);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                fEp[k] = fast_i64_to_f32(Ep[k]);
+                eme[k] = 0;
+            }
+        }
+        // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window).
+        // Pass 1 decides ownership (exact integer coverage tests) into 2-bit codes (0 skip, 1 half,
+        // 2 whole); pass 2 interpolates and accumulates.  Splitting keeps the coverage tests' and the
+        // accumulators' registers apart (occupancy).
+        PHASE_TS(10 + (fEp[0] == 12345.f));
+        if (!(AB & 17) && __builtin_amdgcn_ballot_w64(multi) == 0) {
+            // No clipped face in this wave: ownership and accumulation of the four pairs without
+            // branches.  A neighbour shows my face iff it shows my record (a non-clipped face has exactly
+            // one).  Ownership code: outside the frame 0, background 2, same face 2 for the
+            // lower pixel of the pair / 0 for the upper, else 1 + (q's face covers p) - (p's face covers q).
+            // The pair weight of vertex k is c_d * m_k with m_k = (2 E_k +- 256 A_k (or B_k)) / w_k =
+            // P_k +- Q_k and c_d = code_d * s_d * (W/2 or H/2) / (4D), so the two pairs of an axis fold
+            // into (c_0 + c_1) P_k + (c_0 - c_1) Q_k (and the same with the NDC factors for w).
+            const uint32_t covme = s_cov[kme];
+            float cd[4];
+#pragma unroll
+            for (int dir = 0; dir < 4; ++dir) {
+                const int axis = dir >> 1;
+                const bool me_low = (dir & 1) == 0;
+                const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
+                const int kq = kme + dj * kHalo + di;
+                const int32_t gq = s_gb[kq];
+                const uint32_t covq = s_cov[kq];  // read unconditionally: the code below is all selects
+                const float s = pair_s(axis, me_low ? kme : kq);
+                const int32_t rq = gq & kGbufIndexMask;
+                int code = 1 + (int)((covq >> (dir ^ 1)) & 1u) - (int)((covme >> dir) & 1u);
+                code = rq == rp ? (me_low ? 2 : 0) : code;
+                code = gq < 0 ? 2 : code;
+                code = gq == -2 ? 0 : code;
+                const float K = (axis == 0 ? ns.half_w : ns.half_h) * h2d * 0.5f;
+                cd[dir] = code == 0 ? 0.0f : ((float)code * s) * K;
+            }
+            const float ndc_r = (float)(i + 1) * inv_hw - 1.0f, ndc_l = (float)i * inv_hw - 1.0f;
+            const float ndc_u = (float)(j + 1) * inv_hh - 1.0f, ndc_d = (float)j * inv_hh - 1.0f;
+            const float ux = cd[0] + cd[1], vx = cd[0] - cd[1];
+            const float uwx = cd[0] * ndc_r + cd[1] * ndc_l, vwx = cd[0] * ndc_r - cd[1] * ndc_l;
+            const float uy = cd[2] + cd[3], vy = cd[2] - cd[3];
+            const float uwy = cd[2] * ndc_u + cd[3] * ndc_d, vwy = cd[2] * ndc_u - cd[3] * ndc_d;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float iwk = k == 0 ? iw0 : k == 1 ? iw1 : iw2;
+                const float P = (2.0f * fEp[k]) * iwk;
+                const float Qx = ((float)mA[k] * 256.0f) * iwk, Qy = ((float)mB[k] * 256.0f) * iwk;
+                acc[k * 3 + 0] += ux * P + vx * Qx;
+                acc[k * 3 + 1] += uy * P + vy * Qy;
+                acc[k * 3 + 2] -= (uwx * P + vwx * Qx) + (uwy * P + vwy * Qy);
+            }
+            PHASE_TS(11 + (acc[0] == 12345.f));
+        } else {
+        uint32_t codes = 0;
+#pragma unroll
+        for (int dir = 0; dir < 4; ++dir) {
+            if (AB & 1) break;
+            const int axis = dir >> 1;
+            const bool me_low = (dir & 1) == 0;
+            const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
+            const int kq = kme + dj * kHalo + di;
+            const int32_t gq = s_gb[kq];
+            if (gq == -2) continue;
+            const int klo = me_low ? kme : kq;
+            const float s = pair_s(axis, klo);
+            if (s == 0.0f) continue;
+            const int32_t rq = gq >= 0 ? (gq & kGbufIndexMask) : -1;
+            const int fq = rq >= 0 ? face_of_record(rq, F) : -1;
+            uint32_t code;
+            if (fq == f) {
+                code = me_low ? 2u : 0u;
+            } else if (fq < 0) {
+                code = 2u;
+            } else if (AB & 16) {
+                code = 1u;
+            } else {
+                // the forward's neighbour_coverage(): my face at q (bit dir of p), q's face at p (bit
+                // opposite(dir) of q; opposite flips bit 0 of dir)
+                const bool mine_covers_other = (s_cov[kme] >> dir) & 1u;
+                const bool other_covers_me = (s_cov[kq] >> (dir ^ 1)) & 1u;
+                code = (!mine_covers_other && other_covers_me) ? 2u : (mine_covers_other && !other_covers_me) ? 0u : 1u;
+            }
+            codes |= code << (2 * dir);
+        }
+        PHASE_TS(11 + (codes == 12345u));
+#pragma unroll
+        for (int dir = 0; dir < 4; ++dir) {
+            const uint32_t code = (codes >> (2 * dir)) & 3u;
+            if (code == 0u) continue;
+            const int axis = dir >> 1;
+            const bool me_low = (dir & 1) == 0;
+            const int di = axis == 0 ? (me_low ? 1 : -1) : 0, dj = axis == 1 ? (me_low ? 1 : -1) : 0;
+            const int klo = me_low ? kme : kme + dj * kHalo + di;
+            const float s = pair_s(axis, klo);
+            const float omega = code == 2u ? 1.0f : 0.5f;
+            // midpoint: E(p) + E(q) = 2 E(p) + step, step = one pixel (256 sub-pixels) of the edge
+            float m[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float st = (float)(axis == 0 ? mA[k] : mB[k]) * (me_low ? 256.0f : -256.0f);  // = (float)(A * 256)
+                m[k] = (2.0f * fEp[k] + st) * (k == 0 ? iw0 : k == 1 ? iw1 : iw2);
+            }
+            const int ilo = me_low ? i : i + di, jlo = me_low ? j : j + dj;
+            const float half = axis == 0 ? ns.half_w : ns.half_h;
+            const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
+            const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
+            float g[3];
+            if (!multi) {
+                // Non-clipped face (identity basis, iw_k w_k = 1): lambda_k / Wm = a_k / sum_k (a_k w_k)
+                // = a_k / (2E_0 + 2E_1 + 2E_2 + st_0 + st_1 + st_2) = a_k / (2D), since the edge
+                // functions sum to the constant D and their steps to 0 -- no division per pair
+                const float c = omega * s * half * h2d;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] = c * m[k];
+            } else {
+                float lm[3];
+                if (!fast_lambda(rec(), multi, m[0], m[1], m[2], lm)) continue;
+                // clip w of the parent vertices, read here (clipped faces only) to keep them out of
+                // the registers of the common path
+                const float w0 = sp >= 0 ? T.w[0][sp] : fdata_frame[f].w[0];
+                const float w1 = sp >= 0 ? T.w[1][sp] : fdata_frame[f].w[1];
+                const float w2 = sp >= 0 ? T.w[2][sp] : fdata_frame[f].w[2];
+                const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
+                if (Wm == 0.0f) continue;
+                const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] = tt * lm[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                acc[k * 3 + axis] += g[k];
+                acc[k * 3 + 2] -= g[k] * ndc;
+            }
+        }
+        }
+        // colour weights last: keeps their registers out of the pair loop's live range
+        float lam[3];
+        if (!(AB & 2) && fast_lambda(rec(), multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
+            float Gm[CM];
+#pragma unroll
+            for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * Gm[c];
+        }
+    }
+    if (AB & 4) {
+        float z = 0.0f;
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) z += acc[v];
+        if (z == 1234.5f) grad_verts[t] = z;  // keep the contributions live
+        return;
+    }
+
+    // ---- phase C: segmented sum over runs of equal key along each 16-lane row (one DPP row); the
+    // run tails store their partial sums with plain LDS writes into their slot's contiguous range
+    // (sized in phase A by counting run heads; LDS float atomics serialise on shared addresses); tails
+    // without a slot (table full) or past the partial buffer add straight to global memory
+    const int key = rp >= 0 ? rp : -1;
+    const int start = run_start(key, lx);
+    // 0/1 multipliers: x += shifted(x) * m is one v_fmac with a DPP operand (exact: m is 0 or 1,
+    // contributions are finite)
+    const float mk1 = lx - 1 >= start ? 1.0f : 0.0f, mk2 = lx - 2 >= start ? 1.0f : 0.0f;
+    const float mk4 = lx - 4 >= start ? 1.0f : 0.0f, mk8 = lx - 8 >= start ? 1.0f : 0.0f;
+    if (!(AB & 32)) {
+        // step-major order: each v_fmac_f32_dpp reads a register written >= NVM-1 instructions
+        // earlier (no DPP read-after-write hazard inside the asm)
+        asm volatile("s_nop 1");  // the accumulators may have been written by the last VALU ops
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:1 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk1));
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:2 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk2));
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:4 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk4));
+#pragma unroll
+        for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:8 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk8));
+    }
+    const int kr = dpp_shl_i<1>(key, -3);
+    const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key);
+    float *gvb = grad_verts + (int64_t)b * V * 4;
+    float *gcb = grad_colors + (int64_t)b * V * C;
+    __syncthreads();  // every read of s_G / s_I is done: the union now holds tail partials
+    PHASE_TS(5);
+    int q = -1;
+    if (tail && sp >= 0) {
+        q = atomicAdd(&s_toff[sp], 1);  // the next place in the slot's range
+        if (q >= kTailCap) q = -1;
+    }
+    if (tail) {
+        if (q >= 0) {
+#pragma unroll
+            for (int v = 0; v < NVM; ++v)
+                if (v < NV) s_part[q * NVM + v] = acc[v];
+        } else {
+            const FaceData &fd = fdata_frame[face_of_record(rp, F)];
+            const int32_t vid[3] = {fd.v[0], fd.v[1], fd.v[2]};  // before the atomics (may alias for the compiler)
+#pragma unroll
+            for (int v = 0; v < NVM; ++v) {
+                if (v >= NV || acc[v] == 0.0f) continue;
+                if (v < 9) atomicAdd(gvb + (int64_t)vid[v / 3] * 4 + ((v % 3) == 2 ? 3 : v % 3), acc[v]);
+                else atomicAdd(gcb + (int64_t)vid[(v - 9) / C] * C + (v - 9) % C, acc[v]);
+            }
+        }
+    }
+    __syncthreads();
+    PHASE_TS(6);
+
+    // ---- phase D: flush.  Thread t handles component t % NV of slot t / NV, so every lane of the
+    // workgroup sums one slot's tails in parallel; a slot's components go out as one run of lanes
+    // (~3 cache lines of global float atomics per (tile, record)).
+    const int n = (AB & 8) ? 0 : nslots;
+    const int per_round = 256 / NV;
+    for (int e0 = 0; e0 < n; e0 += per_round) {
+        const int e = e0 + t / NV, comp_id = t - (t / NV) * NV;
+        if (t >= per_round * NV || e >= n) continue;
+        const int kv = comp_id < 9 ? comp_id / 3 : (comp_id - 9) / C;
+        const int vid = T.v[kv][e];
+        // the record's tails are contiguous: four reads in flight per step
+        const int beg = s_lbeg[e], hi = min(beg + s_lcnt[e], kTailCap);
+        float val = 0.0f;
+        for (int q0 = beg; q0 < hi; q0 += 4) {
+            float a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int qq = q0 + u;
+                const float x = s_part[min(qq, hi - 1) * NVM + comp_id];
+                a[u] = qq < hi ? x : 0.0f;
+            }
+            val += (a[0] + a[1]) + (a[2] + a[3]);
+        }
+        if (val == 0.0f) continue;
+        if (AB & 256) {  // ablation: sums without the global atomics
+            if (val == 12345.f) grad_verts[0] = val;
+            continue;
+        }
+        if (comp_id < 9) {
+            const int c3 = comp_id % 3;
+            atomicAdd(gvb + (int64_t)vid * 4 + (c3 == 2 ? 3 : c3), val);
+        } else {
+            atomicAdd(gcb + (int64_t)vid * C + (comp_id - 9) % C, val);
+        }
+    }
+    if (AB & 128) {
+        __syncthreads();
+        PHASE_TS(7);
+    }
+}
