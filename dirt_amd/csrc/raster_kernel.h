@@ -439,6 +439,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             ev[u] = slab_bins[min(idx, slab - 1u)];
         }
     };
+    if (AB & 512) {
+        // ablation: one extra dependent global round trip before the first slab loads (how exposed is the
+        // workgroup's initial load latency?)
+        uint32_t dep = flag[kParQ] & 0u;
+        asm volatile("" : "+v"(dep));
+        slab_bins += dep;
+    }
     if (slab > 0 && !(AB & 8)) load_chunk(0);
     // This forward's setup zeroed the other count set, so the count is the sum of both (no dependent
     // parity load); F == 0: setup did not run
