@@ -101,36 +101,39 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
         Y[k] = (int32_t)__builtin_rintf(yw * 256.0f);
         iwv[k] = iw;
     }
-    int64_t A[3], B[3], C[3];
+    // |X|, |Y| < 2^23 (guard band 16384 px beyond the frame centre, 256 sub-pixels): A, B < 2^24 fit int32
+    // and every product is one 32 x 32 -> 64-bit multiply-add (no 64 x 64 multiplies)
+    int32_t A[3], B[3];
+    int64_t C[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int a = (k + 1) % 3, b = (k + 2) % 3;
-        A[k] = (int64_t)Y[a] - Y[b];
-        B[k] = (int64_t)X[b] - X[a];
-        C[k] = -(A[k] * X[a] + B[k] * Y[a]);
+        A[k] = Y[a] - Y[b];
+        B[k] = X[b] - X[a];
+        C[k] = -((int64_t)A[k] * X[a] + (int64_t)B[k] * Y[a]);
     }
-    const int64_t D = A[0] * X[0] + B[0] * Y[0] + C[0];
-    if (D == 0) { set_empty(out, face); return false; }
-    if (D < 0) {
+    const int64_t D = (int64_t)A[0] * X[0] + (int64_t)B[0] * Y[0] + C[0];
+    // (no early exits: the emptiness tests select at the end, so the divisions below can start while the
+    // integer path is still running -- setup runs one wave per SIMD, where only ILP hides latency)
+    const bool neg = D < 0;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { A[k] = -A[k]; B[k] = -B[k]; C[k] = -C[k]; }
-    }
+    for (int k = 0; k < 3; ++k) { A[k] = neg ? -A[k] : A[k]; B[k] = neg ? -B[k] : B[k]; C[k] = neg ? -C[k] : C[k]; }
     int32_t xmin = min(X[0], min(X[1], X[2])), xmax = max(X[0], max(X[1], X[2]));
     int32_t ymin = min(Y[0], min(Y[1], Y[2])), ymax = max(Y[0], max(Y[1], Y[2]));
-    int64_t i0 = ((int64_t)xmin - 128 + 255) >> 8, i1 = ((int64_t)xmax - 128) >> 8;  // arithmetic shift = floor
-    int64_t j0 = ((int64_t)ymin - 128 + 255) >> 8, j1 = ((int64_t)ymax - 128) >> 8;
+    int32_t i0 = (xmin - 128 + 255) >> 8, i1 = (xmax - 128) >> 8;  // arithmetic shift = floor
+    int32_t j0 = (ymin - 128 + 255) >> 8, j1 = (ymax - 128) >> 8;
     i0 = i0 < 0 ? 0 : i0;
     j0 = j0 < 0 ? 0 : j0;
     i1 = i1 > W - 1 ? W - 1 : i1;
     j1 = j1 > H - 1 ? H - 1 : j1;
-    if (i0 > i1 || j0 > j1) { set_empty(out, face); return false; }
+    const bool nonempty = D != 0 && i0 <= i1 && j0 <= j1;
     const float fx0 = (float)X[0] * 0.00390625f, fy0 = (float)Y[0] * 0.00390625f;
     const float dx1 = (float)X[1] * 0.00390625f - fx0, dy1 = (float)Y[1] * 0.00390625f - fy0;
     const float dx2 = (float)X[2] * 0.00390625f - fx0, dy2 = (float)Y[2] * 0.00390625f - fy0;
     const float dz1 = zw[1] - zw[0], dz2 = zw[2] - zw[0];
     const float det = (float)D * (1.0f / 65536.0f);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { out.A[k] = (int32_t)A[k]; out.B[k] = (int32_t)B[k]; out.C[k] = C[k]; }
+    for (int k = 0; k < 3; ++k) { out.A[k] = A[k]; out.B[k] = B[k]; out.C[k] = C[k]; }
     out.i0 = (uint16_t)i0; out.i1 = (uint16_t)i1; out.j0 = (uint16_t)j0; out.j1 = (uint16_t)j1;
     out.face = face;
     out.fx0 = fx0; out.fy0 = fy0; out.z0 = zw[0];
@@ -142,7 +145,8 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
 #pragma unroll
         for (int i = 0; i < 3; ++i) out.basis[k * 3 + i] = basis[k][i];
     }
-    return true;
+    if (!nonempty) set_empty(out, face);
+    return nonempty;
 }
 
 // R3: exact edge values at pixel centre (i,j)

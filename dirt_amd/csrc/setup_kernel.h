@@ -281,7 +281,25 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         }
         if (fast) {
             const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
-            make_record(tri.v, id, W, H, f, r);
+            if (AB & 2) {
+                // ablation (timing only, wrong records): the pixel bbox of the three vertices without the
+                // record arithmetic (divisions, int64 edge setup, depth plane)
+                const float hw = 0.5f * (float)W, hh = 0.5f * (float)H;
+                float x0 = 1e30f, x1 = -1e30f, y0 = 1e30f, y1 = -1e30f;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float xw = (tri.v[k][0] + 1.0f) * hw, yw = (tri.v[k][1] + 1.0f) * hh;
+                    x0 = fminf(x0, xw); x1 = fmaxf(x1, xw); y0 = fminf(y0, yw); y1 = fmaxf(y1, yw);
+                }
+                // (clamped exactly as make_record does: an empty box stays empty, no index past the frame)
+                const int i0 = (int)fminf(fmaxf(x0, 0.0f), (float)W), i1 = (int)fminf(fmaxf(x1, -1.0f), (float)(W - 1));
+                const int j0 = (int)fminf(fmaxf(y0, 0.0f), (float)H), j1 = (int)fminf(fmaxf(y1, -1.0f), (float)(H - 1));
+                if (i0 <= i1 && j0 <= j1) {
+                    r.i0 = (uint16_t)i0; r.i1 = (uint16_t)i1; r.j0 = (uint16_t)j0; r.j1 = (uint16_t)j1;
+                }
+            } else {
+                make_record(tri.v, id, W, H, f, r);
+            }
             nsub = 1;
             frame_recs[f] = r;
             fbx = (uint32_t)r.i0 | ((uint32_t)r.i1 << 16);
