@@ -85,6 +85,20 @@ __device__ inline void set_empty(Rec &r, int face)
     r.face = face;
 }
 
+// Store a non-clipped face's record without its basis (bytes 92..127; identity, never read for such faces:
+// parent_lambda_f / fast_lambda take the identity branch from FaceData.clipped / the g-buffer's multi bit)
+__device__ __forceinline__ void store_record_fast(Rec *dst, const Rec &r)
+{
+    static_assert(offsetof(Rec, basis) == 92, "Rec layout");
+    const int4 *s4 = reinterpret_cast<const int4 *>(&r);
+    int4 *d4 = reinterpret_cast<int4 *>(dst);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) d4[k] = s4[k];
+    const int *s1 = reinterpret_cast<const int *>(&r) + 20;
+    int *d1 = reinterpret_cast<int *>(dst) + 20;
+    *reinterpret_cast<int3 *>(d1) = *reinterpret_cast<const int3 *>(s1);
+}
+
 // R1..R4 for one (sub-)triangle: fills `out` (a register-resident local), returns true if non-empty.
 __device__ inline bool make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, Rec &out)
 {
@@ -131,7 +145,13 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
     const float dx1 = (float)X[1] * 0.00390625f - fx0, dy1 = (float)Y[1] * 0.00390625f - fy0;
     const float dx2 = (float)X[2] * 0.00390625f - fx0, dy2 = (float)Y[2] * 0.00390625f - fy0;
     const float dz1 = zw[1] - zw[0], dz2 = zw[2] - zw[0];
-    const float det = (float)D * (1.0f / 65536.0f);
+    // (float)D: one conversion when every lane's D fits int32 (the same integer, so the same float)
+    float fD;
+    if (__builtin_amdgcn_ballot_w64(D != (int64_t)(int32_t)D) == 0)
+        fD = (float)(int32_t)D;
+    else
+        fD = (float)D;
+    const float det = fD * (1.0f / 65536.0f);
 #pragma unroll
     for (int k = 0; k < 3; ++k) { out.A[k] = A[k]; out.B[k] = B[k]; out.C[k] = C[k]; }
     out.i0 = (uint16_t)i0; out.i1 = (uint16_t)i1; out.j0 = (uint16_t)j0; out.j1 = (uint16_t)j1;
@@ -191,20 +211,6 @@ __device__ __forceinline__ bool sample_depth(const R &r, int i, int j, uint32_t 
     const uint32_t q = depth_q24(zw);
     if (q >= kDepthMax) return false;
     d = q;
-    return true;
-}
-
-// R6: perspective-correct parent barycentrics from edge values (or sums of two edge values):
-// a_k = E_k / w_k, m_k = a_k * (1 / ((a0 + a1) + a2)) (one correctly rounded division), mapped through the basis
-__device__ __forceinline__ bool parent_lambda(const Rec &r, const int64_t E[3], float lam[3])
-{
-    const float a0 = (float)E[0] * r.iw[0], a1 = (float)E[1] * r.iw[1], a2 = (float)E[2] * r.iw[2];
-    const float s = (a0 + a1) + a2;
-    if (s == 0.0f) return false;
-    const float rs = 1.0f / s;
-    const float m0 = a0 * rs, m1 = a1 * rs, m2 = a2 * rs;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) lam[i] = (m0 * r.basis[i] + m1 * r.basis[3 + i]) + m2 * r.basis[6 + i];
     return true;
 }
 

@@ -301,7 +301,9 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
                 make_record(tri.v, id, W, H, f, r);
             }
             nsub = 1;
-            frame_recs[f] = r;
+            // (the first 92 B: a fast-path record's basis is the identity, and every reader skips it for
+            // non-clipped faces -- 28 % fewer dirty bytes to write back when the kernel ends)
+            store_record_fast(&frame_recs[f], r);
             fbx = (uint32_t)r.i0 | ((uint32_t)r.i1 << 16);
             fby = (uint32_t)r.j0 | ((uint32_t)r.j1 << 16);
             coarse_pairs_add(Q, f, fbx, fby, cshift, count);

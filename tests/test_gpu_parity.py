@@ -336,6 +336,19 @@ def test_fuzz_adversarial_scenes(seed):
         check_scene(*scenes.adversarial_scene(seed, W=W, H=H), seed=seed)
 
 
+def test_extreme_w_and_constant_depth_faces():
+    """Setup's division shortcuts fall back to plain IEEE division outside 2^-60 <= |x| <= 2^60 and for zero
+    numerators: faces whose clip coordinates are scaled by 1e-20 / 1e20 (same projection, w outside the
+    range) and faces of constant depth (zero depth-gradient numerators) must match the oracle bit for bit."""
+    bg, v, c, f = scenes.random_triangles(F=600, W=80, H=64, radius_px=9.0, seed=21)
+    v = v.copy().reshape(-1, 3, 4)
+    scale = np.array([1e-20, 1e20, 1.0, 3e-19, 5e18], np.float32)
+    v *= scale[np.arange(v.shape[0]) % len(scale)][:, None, None]
+    flat = np.arange(v.shape[0]) % 7 == 3
+    v[flat, :, 2] = v[flat, :1, 2] / v[flat, :1, 3] * v[flat, :, 3]  # z/w equal at all three vertices
+    check_scene(bg, v.reshape(-1, 4).astype(np.float32), c, f)
+
+
 def test_session_argument_checks():
     # camera_pos must be a device float32 tensor with the floats the program reads; a procedural
     # session has no gradient (ADVICE r1: the session checked less than the autograd path)
