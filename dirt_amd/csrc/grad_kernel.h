@@ -440,7 +440,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
 #pragma unroll
         for (int c = 0; c < CM; ++c) {
             const float gv = s_G[kme * CP + c];
-            if (c < C) gbq[c] = rp < 0 ? gv : 0.0f;
+            // (non-temporal: nothing in this pipeline reads grad_background back, so its lines need not
+            // stay dirty in L2 for the write-back that ends the launch)
+            if (c < C) __builtin_nontemporal_store(rp < 0 ? gv : 0.0f, &gbq[c]);
         }
     }
 
