@@ -493,7 +493,7 @@ int dirt_debug_setup_ts(int variant, const float *vertices, const int32_t *faces
     case K:                                                                                                   \
         launch_setup<AB>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream);         \
         break
-        V_SETUP(0, 128); V_SETUP(1, 129); V_SETUP(2, 0); V_SETUP(3, 1); V_SETUP(4, 2); V_SETUP(5, 3);
+        V_SETUP(0, 128); V_SETUP(1, 129); V_SETUP(2, 0); V_SETUP(3, 1); V_SETUP(4, 2); V_SETUP(5, 3); V_SETUP(6, 4);
 #undef V_SETUP
     default:
         return fail(DIRT_EINVAL, "dirt_debug_setup_ts: unknown variant");

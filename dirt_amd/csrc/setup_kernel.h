@@ -334,7 +334,10 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     uint32_t *cc = ccount + (int64_t)b * ncoarse * kCountStride;
     for (int c = t; c < ncoarse; c += kBinThreads) {
         const uint32_t n = hist[c];
-        base[c] = (AB & 1) ? 0u : n ? atomicAdd(&cc[c * kCountStride], n) : 0u;  // (AB & 1: ablation, no reservation)
+        // (AB & 1: ablation, no reservation; AB & 4: probe, workgroups split over two counters per tile --
+        // timing only, the raster would not find the second half)
+        const int shard = (AB & 4) ? (int)(blockIdx.x & 1) * 32 : 0;
+        base[c] = (AB & 1) ? 0u : n ? atomicAdd(&cc[c * kCountStride + shard], n) : 0u;
         hist[c] = 0;
     }
     __syncthreads();

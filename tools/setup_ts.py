@@ -33,7 +33,8 @@ def main():
     ms = ctypes.c_float(0)
     nwg = (F + 255) // 256 * B
     for variant, name in ((2, "plain"), (3, "plain, no reservation atomics"), (1, "timestamps, no reservation"),
-                          (4, "no record arithmetic (bbox only)"), (5, "no record arithmetic, no reservation")):
+                          (4, "no record arithmetic (bbox only)"), (5, "no record arithmetic, no reservation"),
+                          (6, "reservation over two counters per tile")):
         tv = []
         for _ in range(20):
             _lib.check(fn(variant, t[1].data_ptr(), t[3].data_ptr(), B, H, W, V, F, sess.saved.data_ptr(),
