@@ -508,12 +508,12 @@ int dirt_debug_setup_ts(int variant, const float *vertices, const int32_t *faces
 }
 
 // Ablation entry point (tools/ablate.py): the backward with parts of grad_kernel switched off.
-// Not part of include/dirt_mi355x.h; C == 3 only.  Returns the kernel time in ms (hipEvents).
+// Not part of include/dirt_mi355x.h; C == 3 or 7.  Returns the kernel time in ms (hipEvents).
 int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
                            const void *saved, int B, int H, int W, int C, int V, int F, float *grad_vertices,
                            float *grad_vertex_colors, float *grad_background, void *stream_, float *ms)
 {
-    if (C != 3) return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: C must be 3");
+    if (C != 3 && C != 7) return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: C must be 3 or 7");
     Layout L;
     int rc = make_layout(B, H, W, F, 0, L);
     if (rc) return rc;
@@ -531,10 +531,14 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     dim3 grid((unsigned)L.ntiles, (unsigned)B);
 #define V_GRAD(AB)                                                                                                   \
     case AB:                                                                                                         \
-        grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W,\
-                                                           C, V,                                                     \
-                                                           F, tile_grid(L.ntx), L.nrec, grad_vertices, grad_vertex_colors,     \
-                                                           grad_background, ndc_scale(W, H));                        \
+        if (C == 3)                                                                                                  \
+            grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, \
+                                                               H, W, C, V, F, tile_grid(L.ntx), L.nrec, grad_vertices, \
+                                                               grad_vertex_colors, grad_background, ndc_scale(W, H));  \
+        else                                                                                                         \
+            grad_kernel<7, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, \
+                                                               H, W, C, V, F, tile_grid(L.ntx), L.nrec, grad_vertices, \
+                                                               grad_vertex_colors, grad_background, ndc_scale(W, H));  \
         break
     switch (variant) {
         V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);

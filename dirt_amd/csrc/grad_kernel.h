@@ -195,6 +195,19 @@ __device__ __forceinline__ float pair_scalar(const int32_t *s_gb, const float *s
         a = (Gp.x + Gq.x) * (Iq.x - Ip.x);
         a = a + (Gp.y + Gq.y) * (Iq.y - Ip.y);
         a = a + (Gp.z + Gq.z) * (Iq.z - Ip.z);
+    } else if constexpr (CP == 8) {
+        // 5..8 channels at a 32-B stride: each operand is two ds_read_b128 instead of C ds_read_b32
+        float Gp[8], Gq[8], Ip[8], Iq[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            *reinterpret_cast<float4 *>(&Gp[4 * h]) = *reinterpret_cast<const float4 *>(&s_G[k * 8 + 4 * h]);
+            *reinterpret_cast<float4 *>(&Gq[4 * h]) = *reinterpret_cast<const float4 *>(&s_G[k2 * 8 + 4 * h]);
+            *reinterpret_cast<float4 *>(&Ip[4 * h]) = *reinterpret_cast<const float4 *>(&s_I[k * 8 + 4 * h]);
+            *reinterpret_cast<float4 *>(&Iq[4 * h]) = *reinterpret_cast<const float4 *>(&s_I[k2 * 8 + 4 * h]);
+        }
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < C) a += (Gp[c] + Gq[c]) * (Iq[c] - Ip[c]);
     } else {
         for (int c = 0; c < C; ++c) a += (s_G[k * CP + c] + s_G[k2 * CP + c]) * (s_I[k2 * CP + c] - s_I[k * CP + c]);
     }
@@ -228,7 +241,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                                                    const NdcScale ns)
 {
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
-    constexpr int CP = CM == 3 ? 4 : CM;  // LDS pixel stride (float4 for RGB)
+    // LDS pixel stride: float4 for RGB, two float4 for 5..8 channels (wide LDS reads)
+    constexpr int CP = CM == 3 ? 4 : (CM > 4 && CM <= 8) ? 8 : CM;
     constexpr int NVM = 9 + 3 * CM;
     const int C = CC > 0 ? CC : Cdyn;
     const int NV = 9 + 3 * C;
@@ -333,6 +347,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             if constexpr (CM == 3) {
                 *reinterpret_cast<float4 *>(&s_G[k * CP]) = make_float4(Gv[u][0], Gv[u][1], Gv[u][2], 0.0f);
                 *reinterpret_cast<float4 *>(&s_I[k * CP]) = make_float4(Iv[u][0], Iv[u][1], Iv[u][2], 0.0f);
+            } else if constexpr (CP == 8) {
+                float g8[8], i8[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    g8[c] = c < CM && c < C ? Gv[u][c < CM ? c : 0] : 0.0f;
+                    i8[c] = c < CM && c < C ? Iv[u][c < CM ? c : 0] : 0.0f;
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    *reinterpret_cast<float4 *>(&s_G[k * 8 + 4 * h]) = *reinterpret_cast<const float4 *>(&g8[4 * h]);
+                    *reinterpret_cast<float4 *>(&s_I[k * 8 + 4 * h]) = *reinterpret_cast<const float4 *>(&i8[4 * h]);
+                }
             } else {
 #pragma unroll
                 for (int c = 0; c < CM; ++c)

@@ -102,6 +102,14 @@ def test_shared_vertex_mesh():
     check_scene(*scenes.shared_mesh_scene())
 
 
+@pytest.mark.parametrize("C", [1, 5, 7, 8])
+def test_shared_vertex_mesh_vertex_aggregated_flush(C):
+    """Non-RGB backward kernels sum each tile's contributions per vertex in LDS before the global atomics
+    (grad_kernel.h VertexTable); the generic 5- and 8-channel paths also take the 32-B LDS stride."""
+    check_scene(*scenes.shared_mesh_scene(C=C))
+    check_scene(*scenes.shared_mesh_scene(W=160, H=120, C=C, seed=9, n=40))
+
+
 def test_single_channel_and_seven_channels():
     check_scene(*scenes.random_triangles(F=300, W=64, H=48, C=1, radius_px=10.0, seed=2))
     check_scene(*scenes.random_triangles(F=300, W=64, H=48, C=7, radius_px=10.0, seed=3))

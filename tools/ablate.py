@@ -1,4 +1,8 @@
-"""Interleaved A/B timing of grad_kernel ablation variants (one process, median of N rounds)."""
+"""Interleaved A/B timing of grad_kernel ablation variants (one process, median of N rounds).
+
+    python tools/ablate.py          # config 3 (50k random triangles, 1024^2 x 3): backward and raster
+    python tools/ablate.py c4       # config 4 (20k-tri shared-vertex mesh, 512^2 x 7): backward only
+"""
 import ctypes
 import os
 import sys
@@ -19,7 +23,11 @@ NAMES = {0: "full", 1: "no pairs", 2: "no colour", 3: "no pairs+colour", 4: "no 
 
 def main():
     dev = torch.device("cuda", 0)
-    bg, v, c, f = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
+    which = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    if which == "c4":
+        bg, v, c, f = scenes.deferred_mesh_scene()
+    else:
+        bg, v, c, f = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
     t = [torch.from_numpy(a[None]).to(dev) for a in (bg, v, c, f)]
     B, H, W, C = t[0].shape
     V, F = t[1].shape[1], t[3].shape[1]
@@ -43,6 +51,8 @@ def main():
                 res[k].append(ms.value * 1e3)
     for k, name in NAMES.items():
         print("grad   %-28s median %8.2f us  min %8.2f" % (name, np.median(res[k]), np.min(res[k])))
+    if C != 3:
+        return  # the raster variants are instantiated for C = 3 only
     rfn = lib.dirt_debug_raster_variant
     rfn.argtypes = [ctypes.c_int, P, P, P, P] + [ctypes.c_int] * 6 + [P, P, P, P, P, ctypes.POINTER(ctypes.c_float)]
     rfn.restype = ctypes.c_int

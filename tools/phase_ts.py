@@ -1,4 +1,4 @@
-"""Per-phase timestamps of the instrumented backward (grad_kernel<3,128>) at config 3.
+"""Per-phase timestamps of the instrumented backward (grad_kernel<3,128>) at config 3 (`c4` argument: config 4).
 
 Prints the median / p90 duration of each phase per workgroup, the workgroup lifetime, and how many
 workgroups were resident per CU on average (from HW_ID / XCC_ID)."""
@@ -21,7 +21,10 @@ PH = ["load gb/G/I", "scalars+own inserts", "ring inserts", "slot record loads",
 
 def main():
     dev = torch.device("cuda", 0)
-    bg, v, c, f = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
+    if len(sys.argv) > 1 and sys.argv[1] == "c4":  # config 4: shared-vertex mesh, 512^2 x 7 (grad_kernel<7,128>)
+        bg, v, c, f = scenes.deferred_mesh_scene()
+    else:
+        bg, v, c, f = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
     t = [torch.from_numpy(a[None]).to(dev) for a in (bg, v, c, f)]
     B, H, W, C = t[0].shape
     V, F = t[1].shape[1], t[3].shape[1]
