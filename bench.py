@@ -114,10 +114,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # DIRT_BENCH_SHARED_GPU=1: rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks share
+    # cuda:LOCAL_RANK % count, timing reduced over gloo); the driver's multi-GPU runs leave it unset (RCCL)
+    shared = os.environ.get("DIRT_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local_rank %= max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
 
@@ -168,7 +176,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -196,6 +204,17 @@ def main():
                 "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic is not None else None,
                 "alg_bytes_per_launch": kbytes[dom], "avg_us": round(kern_us[dom], 2),
                 "op_frac": round((fwd_b + bwd_b) / (ms_per_step * 1e-3 / world) / 1e9 / HBM_PEAK_GBS, 4)}
+    # the op's algorithmic bytes over each pass's kernel time (fwd = setup + raster, bwd =
+    # grad), and the measured HBM bytes (rocprof PMC, traffic.json) of the dominant kernel over its time --
+    # the north-star's "HBM bandwidth on the backward scatter" is stated on measured bytes
+    t_fwd = kern_us.get("setup_kernel", 0.0) + kern_us.get("raster_kernel", 0.0)
+    t_bwd = kern_us.get("grad_kernel", 0.0)
+    if t_fwd > 0:
+        roofline["fwd_frac"] = round(fwd_b / (t_fwd * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    if t_bwd > 0:
+        roofline["bwd_frac"] = round(bwd_b / (t_bwd * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    if traffic is not None:
+        roofline["traffic_frac"] = round(traffic / (kern_us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
 
     cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
