@@ -110,6 +110,14 @@ def test_shared_vertex_mesh_vertex_aggregated_flush(C):
     check_scene(*scenes.shared_mesh_scene(W=160, H=120, C=C, seed=9, n=40))
 
 
+@pytest.mark.parametrize("C", [2, 5, 7])
+def test_clipping_wide_channel_stride(C):
+    """Clipped faces (the backward's general pair path) and the 2..8-channel kernels with G / I staged at
+    the 32-B LDS stride."""
+    check_scene(*scenes.clipping_scene(C=C))
+    check_scene(*scenes.random_triangles(F=400, W=72, H=56, C=C, radius_px=12.0, seed=30 + C, perspective=True))
+
+
 def test_single_channel_and_seven_channels():
     check_scene(*scenes.random_triangles(F=300, W=64, H=48, C=1, radius_px=10.0, seed=2))
     check_scene(*scenes.random_triangles(F=300, W=64, H=48, C=7, radius_px=10.0, seed=3))
