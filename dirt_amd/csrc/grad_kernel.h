@@ -424,15 +424,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
         // bottom row of the halo (their one pair into the tile); nothing reads the others
         if constexpr (!kRecompute) {
-        const int rt = (t & 63) * 4 + (t >> 6);
         s_sx[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + 1, C);
         s_sy[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + kHalo, C);
-        if (rt < 16) {
-            const int k = (rt + 1) * kHalo;  // (0, rt + 1)
-            s_sx[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + 1, C);
-        } else if (rt < 32) {
-            const int k = rt - 15;  // (rt - 15, 0)
-            s_sy[k] = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + kHalo, C);
+        if (t >= 224) {
+            // the 32 halo pairs into the tile, one per lane of the last wave and one pair_scalar for all
+            // of them (the LDS reads of a pair are wide: spreading them over every wave, or a branch per
+            // axis, would cost each wave two more rounds of them)
+            const int h = t - 224;
+            const bool xa = h < 16;
+            const int k = xa ? (h + 1) * kHalo : h - 15;  // (0, h + 1) or (h - 15, 0)
+            const float sv = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + (xa ? 1 : kHalo), C);
+            if (xa) s_sx[k] = sv;
+            else s_sy[k] = sv;
         }
         }
         if (filler) {
