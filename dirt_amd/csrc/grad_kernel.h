@@ -373,10 +373,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     PHASE_TS(1);
     const int32_t gp = in_frame ? s_gb[kme] : -2;
     {
-        const int rt = (t & 63) * 4 + (t >> 6);  // 0..255 spread over the four waves
         // the tile's own records (run heads only; all distinct keys may not fit: the rest read global
         // memory).  The halo's records are not needed: pair coverage comes from the forward's bits.
-        (void)rt;
         const int32_t g = s_gb[kme];
         const int key = g >= 0 ? g : -1;
         const int start = run_start(key, lx);
