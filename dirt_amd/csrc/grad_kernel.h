@@ -736,10 +736,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     // workgroup sums one slot's tails in parallel; a slot's components go out as one run of lanes
     // (~3 cache lines of global float atomics per (tile, record)).
     const int n = (AB & 8) ? 0 : nslots;
-    const int per_round = 256 / NV;
+    // whole records per wave: no record's components straddle two waves, so each record's atomics leave
+    // in one wave instruction (the cache lines one atomic instruction touches are what it costs)
+    const int rpw = 64 / NV, per_round = 4 * rpw;
+    const int wl = t & 63;
     for (int e0 = 0; e0 < n; e0 += per_round) {
-        const int e = e0 + t / NV, comp_id = t - (t / NV) * NV;
-        if (t >= per_round * NV || e >= n) continue;
+        const int e = e0 + (t >> 6) * rpw + wl / NV, comp_id = wl - (wl / NV) * NV;
+        if (wl >= rpw * NV || e >= n) continue;
         const int kv = comp_id < 9 ? comp_id / 3 : (comp_id - 9) / C;
         const int vid = T.v[kv][e];
         // the record's tails are contiguous: four reads in flight per step
