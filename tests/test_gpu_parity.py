@@ -7,6 +7,8 @@ Tolerances:
   * grad_vertex_colors, grad_vertices: fp32 atomics sum in arbitrary order ->
         |gpu - oracle| <= 1e-4 * |oracle| + 1e-5 * scale, scale = max|oracle| (per tensor)
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -333,14 +335,16 @@ def test_deep_depth_complexity_culling(perspective):
     check_scene(bg, v2, c2, f2)
 
 
-@pytest.mark.parametrize("seed", range(36))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUZZ_SEEDS", "36"))))
 def test_fuzz_adversarial_scenes(seed):
     """Raster-rule edge cases mixed at random (scenes.adversarial_scene): pixel-centre / pixel-edge
     vertices, slivers, sub-pixel triangles, duplicate and coplanar faces, near / far / w <= 0 clipping,
-    guard-band overflow; three frame shapes, one batch of two."""
+    guard-band overflow; three frame shapes, one batch of two.  DIRT_FUZZ_SEEDS=N runs N seeds (the
+    default suite runs 36); seeds past 36 also cycle the channel count over 3, 7, 1, 5."""
     W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
+    C = 3 if seed < 36 else (3, 7, 1, 5)[seed % 4]
     if seed % 4 == 3:
-        frames = [scenes.adversarial_scene(seed * 10 + k, W=W, H=H, F=150) for k in range(2)]
+        frames = [scenes.adversarial_scene(seed * 10 + k, W=W, H=H, C=C, F=150) for k in range(2)]
         F = max(fr[3].shape[0] for fr in frames)
         # pad the shorter frame with degenerate faces so both frames share F
         frames = [(bg, v, c, np.concatenate([f, np.zeros((F - f.shape[0], 3), np.int32)])) for bg, v, c, f in frames]
@@ -349,7 +353,7 @@ def test_fuzz_adversarial_scenes(seed):
                    np.concatenate([c, np.tile(c[:1], (V - c.shape[0], 1))]), f) for bg, v, c, f in frames]
         check_scene(*[np.stack([fr[k] for fr in frames]) for k in range(4)], seed=seed)
     else:
-        check_scene(*scenes.adversarial_scene(seed, W=W, H=H), seed=seed)
+        check_scene(*scenes.adversarial_scene(seed, W=W, H=H, C=C), seed=seed)
 
 
 def test_extreme_w_and_constant_depth_faces():
