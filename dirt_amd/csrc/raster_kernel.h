@@ -43,7 +43,8 @@ struct TileGrid {
     uint32_t inv;
     __device__ __forceinline__ void split(int tile, int &tx, int &ty) const
     {
-        ty = (int)__umulhi((uint32_t)tile, inv);
+        // (ntx == 1: the reciprocal 2^32 does not fit in 32 bits and tile_grid stores 0; every tile is a row)
+        ty = ntx == 1 ? tile : (int)__umulhi((uint32_t)tile, inv);
         tx = tile - ty * ntx;
     }
 };

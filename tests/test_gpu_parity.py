@@ -304,6 +304,14 @@ def test_config4_deferred_gbuffer_7_channels():
     check_scene(*scenes.deferred_mesh_scene())
 
 
+@pytest.mark.parametrize("H,W", [(1, 1), (1, 17), (17, 1), (15, 15), (16, 33), (65, 63)])
+def test_tiny_and_odd_frames(H, W):
+    """Frames smaller than one tile or one coarse tile, and sizes that are not multiples of the tile."""
+    for C in (1, 3):
+        check_scene(*scenes.random_triangles(F=60, W=W, H=H, C=C, radius_px=max(2.0, min(W, H) / 2.0),
+                                             seed=H * 100 + W + C))
+
+
 @pytest.mark.parametrize("H,W", [(40, 8192), (8192, 24)])
 def test_maximum_frame_dimensions(H, W):
     """DIRT_MAX_DIM = 8192 along each axis: tile, coarse-bin and row-flip indexing at the extremes."""
