@@ -1,0 +1,36 @@
+"""Frame-size sweep (GPU vs oracle, tests/test_gpu_parity.check_scene): every failure is printed.
+
+    python tools/debug/size_sweep.py
+"""
+import os
+import sys
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+import scenes  # noqa: E402
+from test_gpu_parity import check_scene  # noqa: E402
+
+rng = np.random.default_rng(123)
+sizes = [(h, w) for h in (1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 129) for w in (1, 3, 16, 17, 33, 64, 65, 130)]
+sizes += [(int(a), int(b)) for a, b in rng.integers(1, 700, size=(40, 2))]
+bad = 0
+for k, (H, W) in enumerate(sizes):
+    C = (1, 3, 7)[k % 3]
+    B = 1 + (k % 4 == 0)
+    try:
+        frames = [scenes.random_triangles(F=int(rng.integers(0, 400)) if b == 0 else 0, W=W, H=H, C=C,
+                                          radius_px=float(rng.uniform(1.0, 40.0)), seed=k * 10 + b,
+                                          perspective=bool(k % 2)) for b in range(B)]
+        F = max(fr[3].shape[0] for fr in frames)
+        if F == 0:
+            continue
+        frames = [scenes.random_triangles(F=F, W=W, H=H, C=C, radius_px=float(rng.uniform(1.0, 40.0)),
+                                          seed=k * 10 + b, perspective=bool(k % 2)) for b in range(B)]
+        check_scene(*[np.stack([fr[j] for fr in frames]) for j in range(4)], seed=k)
+    except Exception as e:  # noqa: BLE001
+        bad += 1
+        print("FAIL H=%d W=%d C=%d B=%d: %s" % (H, W, C, B, str(e).splitlines()[0][:200]))
+print("sizes", len(sizes), "bad", bad)
