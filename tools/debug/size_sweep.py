@@ -20,6 +20,7 @@ bad = 0
 for k, (H, W) in enumerate(sizes):
     C = (1, 3, 7)[k % 3]
     B = 1 + (k % 4 == 0)
+    cap = 0
     try:
         frames = [scenes.random_triangles(F=int(rng.integers(0, 400)) if b == 0 else 0, W=W, H=H, C=C,
                                           radius_px=float(rng.uniform(1.0, 40.0)), seed=k * 10 + b,
@@ -29,8 +30,9 @@ for k, (H, W) in enumerate(sizes):
             continue
         frames = [scenes.random_triangles(F=F, W=W, H=H, C=C, radius_px=float(rng.uniform(1.0, 40.0)),
                                           seed=k * 10 + b, perspective=bool(k % 2)) for b in range(B)]
-        check_scene(*[np.stack([fr[j] for fr in frames]) for j in range(4)], seed=k)
+        cap = int(rng.integers(1, 24)) if k % 3 == 1 else 0  # every third size: tiny slabs (overflow path)
+        check_scene(*[np.stack([fr[j] for fr in frames]) for j in range(4)], seed=k, bin_capacity=cap)
     except Exception as e:  # noqa: BLE001
         bad += 1
-        print("FAIL H=%d W=%d C=%d B=%d: %s" % (H, W, C, B, str(e).splitlines()[0][:200]))
+        print("FAIL H=%d W=%d C=%d B=%d cap=%d: %s" % (H, W, C, B, cap, str(e).splitlines()[0][:200]))
 print("sizes", len(sizes), "bad", bad)
