@@ -209,3 +209,19 @@ def test_hill_overlap_and_mesh():
     rpx, rgb, _ = oracle.hill_fwd(T, v[None], f[None], 3, cam)
     np.testing.assert_array_equal(gb, rgb)
     np.testing.assert_array_equal(px, rpx)
+
+
+@pytest.mark.parametrize("sid", [1, 2, 3, 4, 5, 6])
+def test_programs_on_narrow_and_odd_frames(sid):
+    """Every depth-tested fragment program on frames one tile column wide and on odd sizes (the tile-row
+    split for a single tile column was wrong until the end of round 2)."""
+    from dirt_amd import rasterise_ops
+    cam = np.array(list(CAMS["square_test"]) + [0.3, 0.05, 0.5, 0.0, -0.4, 0.01, 0.0, 0.02], np.float32)
+    for (H, W) in [(40, 9), (17, 33), (23, 1)]:
+        bg, v, c, f = fullscreen(H, W)
+        t = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (bg, v, c, f)]
+        px, gb = rasterise_ops._rasterise_batched(*t, torch.from_numpy(cam).cuda(), H, W, bg.shape[-1], sid,
+                                                  return_gbuffer=True)
+        rpx, rgb, _ = oracle.rasterise_fwd(bg, v, c, f, shader_id=sid, camera_pos=cam)
+        np.testing.assert_array_equal(gb.cpu().numpy(), rgb)
+        np.testing.assert_array_equal(px.cpu().numpy(), rpx)
