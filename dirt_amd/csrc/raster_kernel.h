@@ -43,14 +43,15 @@ struct TileGrid {
     uint32_t inv;
     __device__ __forceinline__ void split(int tile, int &tx, int &ty) const
     {
-        // (ntx == 1: the reciprocal 2^32 does not fit in 32 bits and tile_grid stores 0; every tile is a row)
-        ty = ntx == 1 ? tile : (int)__umulhi((uint32_t)tile, inv);
+        // floor(tile / ntx) = umulhi(2 tile, ceil(2^31 / ntx)), exact for tile < 2^18, ntx <= 512; the
+        // 2^31 scale keeps the reciprocal of ntx = 1 in 32 bits (2^32 / 1 would not fit)
+        ty = (int)__umulhi((uint32_t)tile << 1, inv);
         tx = tile - ty * ntx;
     }
 };
 static_assert((DIRT_MAX_DIM / kTile) <= 512 && (DIRT_MAX_DIM / kTile) * (DIRT_MAX_DIM / kTile) <= (1 << 18),
               "TileGrid reciprocal range");
-inline TileGrid tile_grid(int ntx) { return TileGrid{ntx, (uint32_t)(((1ull << 32) + (uint64_t)ntx - 1) / (uint64_t)ntx)}; }
+inline TileGrid tile_grid(int ntx) { return TileGrid{ntx, (uint32_t)(((1ull << 31) + (uint64_t)ntx - 1) / (uint64_t)ntx)}; }
 
 #ifndef DIRT_RASTER_LISTS
 #define DIRT_RASTER_LISTS 1  // per-wave entry lists (1) or the scalar bit-mask walk (0)
