@@ -500,3 +500,24 @@ def test_repeated_forwards_batch_of_large_frames_identical():
         assert torch.equal(px, outs[0][0]) and torch.equal(gb, outs[0][1])
     ref_px, ref_gb, _ = oracle.rasterise_fwd(host[0][:1], host[1][:1], host[2][:1], host[3][:1])
     assert np.array_equal(outs[0][0][:1].cpu().numpy(), ref_px)
+
+
+def test_backward_accumulate_flag_adds_and_overwrite_resets():
+    """DIRT_BWD_ACCUMULATE (include/dirt_mi355x.h): a second backward adds into grad_vertices /
+    grad_vertex_colors and overwrites grad_background; the autograd path (flags 0) overwrites all three."""
+    from dirt_amd.session import RasteriseSession
+    bg, v, c, f = (torch.from_numpy(a[None]).cuda() for a in scenes.random_triangles(F=500, W=96, H=80, seed=41))
+    B, H, W, C = bg.shape
+    sess = RasteriseSession(B, H, W, C, v.shape[1], f.shape[1], device="cuda")
+    sess.forward(bg, v, c, f)
+    g = torch.randn_like(sess.pixels)
+    gbg1, gv1, gc1 = (t.clone() for t in sess.backward(g))
+    gbg2, gv2, gc2 = sess.backward(g)
+    torch.testing.assert_close(gv2, 2 * gv1, rtol=1e-5, atol=1e-5 * float(gv1.abs().max()))
+    torch.testing.assert_close(gc2, 2 * gc1, rtol=1e-5, atol=1e-5 * float(gc1.abs().max()))
+    assert torch.equal(gbg2, gbg1)
+    # the next forward zero-fills the accumulators again: one backward gives the single result
+    sess.forward(bg, v, c, f)
+    gbg3, gv3, gc3 = sess.backward(g)
+    torch.testing.assert_close(gv3, gv1, rtol=1e-5, atol=1e-5 * float(gv1.abs().max()))
+    torch.testing.assert_close(gc3, gc1, rtol=1e-5, atol=1e-5 * float(gc1.abs().max()))
