@@ -163,7 +163,7 @@ def _hill_gpu(T, v, f, C, cam):
 def test_hill_bit_exact(name):
     v, f = scenes.fullscreen_quad()
     cam = hill_cam(HILL_CAMS[name])
-    for (H, W) in ((54, 96), (64, 64)):
+    for (H, W) in ((54, 96), (64, 64), (40, 9), (23, 2)):  # (the last two: one tile column)
         for Ct, C in ((4, 3), (1, 1), (3, 4)):
             T = scenes.hill_terrain(H, W, Ct)[None]
             px, gb = _hill_gpu(T, v[None], f[None], C, cam)
