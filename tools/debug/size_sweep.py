@@ -36,3 +36,24 @@ for k, (H, W) in enumerate(sizes):
         bad += 1
         print("FAIL H=%d W=%d C=%d B=%d cap=%d: %s" % (H, W, C, B, cap, str(e).splitlines()[0][:200]))
 print("sizes", len(sizes), "bad", bad)
+
+# random-index meshes: arbitrary vertex sharing, repeated indices (degenerate faces), V unrelated to F
+bad2 = 0
+for k in range(60):
+    H, W = (int(x) for x in rng.integers(1, 300, size=2))
+    C = (1, 3, 7)[k % 3]
+    V = int(rng.integers(3, 2000))
+    F = int(rng.integers(1, 1500))
+    w = rng.uniform(0.5, 2.0, size=(V, 1)) if k % 2 else np.ones((V, 1))
+    xy = rng.uniform(-1.3, 1.3, size=(V, 2)) * w
+    z = rng.uniform(-1.1, 1.1, size=(V, 1)) * w
+    v = np.concatenate([xy, z, w], 1).astype(np.float32)
+    f = rng.integers(0, V, size=(F, 3)).astype(np.int32)
+    c = rng.uniform(0, 1, size=(V, C)).astype(np.float32)
+    bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
+    try:
+        check_scene(bg, v, c, f, seed=k)
+    except Exception as e:  # noqa: BLE001
+        bad2 += 1
+        print("FAIL mesh H=%d W=%d C=%d V=%d F=%d: %s" % (H, W, C, V, F, str(e).splitlines()[0][:200]))
+print("random-index meshes 60 bad", bad2)
