@@ -521,3 +521,16 @@ def test_backward_accumulate_flag_adds_and_overwrite_resets():
     gbg3, gv3, gc3 = sess.backward(g)
     torch.testing.assert_close(gv3, gv1, rtol=1e-5, atol=1e-5 * float(gv1.abs().max()))
     torch.testing.assert_close(gc3, gc1, rtol=1e-5, atol=1e-5 * float(gc1.abs().max()))
+
+
+@pytest.mark.parametrize("C,r", [(3, 0.6), (7, 1.0), (1, 1.5)])
+def test_dense_tiles_slot_table_and_tail_overflow(C, r):
+    """Tiles showing more distinct records than the backward's 64-slot LDS table, with more row runs than
+    its LDS tail buffer holds: both fall back to global memory (grad_kernel.h kNoSlot, q >= kTailCap)."""
+    bg, v, c, f = scenes.random_triangles(F=30000, W=64, H=48, C=C, radius_px=r, seed=int(r * 10) + C)
+    _, gb, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
+    g = gb[0]
+    per_tile = [len(np.unique(g[y:y + 16, x:x + 16][g[y:y + 16, x:x + 16] >= 0]))
+                for y in range(0, 48, 16) for x in range(0, 64, 16)]
+    assert max(per_tile) > 64
+    check_scene(bg, v, c, f)
