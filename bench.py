@@ -61,9 +61,41 @@ def make_inputs(cfg, rank, device):
     return host, dev, torch.from_numpy(g).to(device), g
 
 
+def host_cpu_info():
+    """What the CPU baseline ran on: the threads it used, the box's online CPUs and this process's affinity,
+    and the lscpu model name."""
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.lower().startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:  # lscpu absent: report what Python knows
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc_online": os.cpu_count(), "affinity_cpus": affinity}
+
+
+def cpu_threads():
+    """Every host core this job may use: the CPU share the pool grants one GPU's job (OMP_NUM_THREADS, which
+    the GPU box sets; the box's rules size worker pools to that share), else the process's affinity mask."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        return env
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(host, grad_host, budget_s=10.0, max_reps=20):
     from oracle import oracle
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    nthreads = cpu_threads()
     bg, v, c, f = host
     B, H, W, C = bg.shape
     times = []
@@ -74,10 +106,12 @@ def cpu_baseline(host, grad_host, budget_s=10.0, max_reps=20):
         grads = oracle.rasterise_bwd(v, c, f, px, grad_host, gb, nthreads=nthreads)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
-    return {"value": B * H * W / t / 1e6, "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
-            "sample": "%d x full config frame(s) (%dx%dx%d, F=%d) fwd+bwd, median of %d reps, oracle/dirt_oracle.c "
-                      "OpenMP" % (B, H, W, C, f.shape[1], len(times)),
-            "ms_per_frame": t * 1e3 / B}, (px, gb) + tuple(grads)
+    out = {"value": B * H * W / t / 1e6, "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
+           "sample": "%d x full config frame(s) (%dx%dx%d, F=%d) fwd+bwd, median of %d reps, oracle/dirt_oracle.c "
+                     "OpenMP, %d threads" % (B, H, W, C, f.shape[1], len(times), nthreads),
+           "ms_per_frame": t * 1e3 / B}
+    out.update(host_cpu_info())
+    return out, (px, gb) + tuple(grads)
 
 
 def parity(sess, ref):
@@ -96,6 +130,39 @@ def parity(sess, ref):
     return out
 
 
+def graph_of(fn, n, stream):
+    """Capture n calls of fn into one HIP graph on `stream` (warmed on the same stream first, so cached
+    workspaces keyed by stream are hit instead of allocated inside the capture)."""
+    with torch.cuda.stream(stream):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        for _ in range(n):
+            fn()
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    return g
+
+
+def timed(run, n_calls, barrier, world, device, shared):
+    """Run `run` n_calls times between barrier + synchronize on both sides; max over ranks (seconds)."""
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_calls):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,13 +176,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--profile-steps", type=int, default=50)
+    ap.add_argument("--rotate", type=int, default=4,
+                    help="extra leg: rotate this many distinct frames (inputs, outputs, workspaces) so the step's "
+                         "working set exceeds the 256 MiB Infinity Cache; 0 = skip")
+    ap.add_argument("--no-api-leg", action="store_true", help="skip the public rasterise_batch + autograd leg")
+    ap.add_argument("--no-gather-leg", action="store_true", help="N > 1: skip the RCCL all-gather leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # DIRT_BENCH_SHARED_GPU=1: rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks share
-    # cuda:LOCAL_RANK % count, timing reduced over gloo); the driver's multi-GPU runs leave it unset (RCCL)
+    # cuda:LOCAL_RANK % count, collectives over gloo); the driver's multi-GPU runs leave it unset (RCCL)
     shared = os.environ.get("DIRT_BENCH_SHARED_GPU") == "1"
     if shared:
         local_rank %= max(1, torch.cuda.device_count())
@@ -137,10 +209,15 @@ def main():
     V = 3 * F
     host, (bg, v, c, f), grad, grad_host = make_inputs(cfg, rank, device)
     sess = RasteriseSession(B, H, W, C, V, F, device=device)
+    cap_stream = torch.cuda.Stream(device)
 
     def step():
         sess.forward(bg, v, c, f)
         sess.backward(grad)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -149,47 +226,33 @@ def main():
     # remainder eagerly
     gs = 1 if args.no_graph else max(1, min(args.graph_steps, args.steps))
     n_replays, n_rest = divmod(args.steps, gs)
-    run = step
-    if not args.no_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for _ in range(gs):
-                step()
-        for _ in range(2):
-            graph.replay()
-        run = graph.replay
-    else:
+    if args.no_graph:
         n_replays, n_rest = args.steps, 0
+        run = step
+    else:
+        run = graph_of(step, gs, cap_stream).replay
 
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
+    def timed_loop():
+        for _ in range(n_replays):
+            run()
+        for _ in range(n_rest):
+            step()
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(n_replays):
-        run()
-    for _ in range(n_rest):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else device)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(timed_loop, 1, barrier, world, device, shared)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * B * H * W * args.steps / elapsed / 1e6
 
     # per-kernel HIP-event timing (same kernels, eager launches, outside the timed loop)
-    _lib.profile_enable(True)
-    for _ in range(args.profile_steps):
-        step()
-    torch.cuda.synchronize()
-    prof = _lib.profile_read()
-    _lib.profile_enable(False)
-    kern_us = {k: (ms / n * 1e3 if n else 0.0) for k, (n, ms) in prof.items()}
+    def kernel_times(fn, n):
+        _lib.profile_enable(True)
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        prof = _lib.profile_read()
+        _lib.profile_enable(False)
+        return {k: (ms / cnt * 1e3 if cnt else 0.0) for k, (cnt, ms) in prof.items()}
+
+    kern_us = kernel_times(step, args.profile_steps)
     kbytes, fwd_b, bwd_b = alg_bytes(B, H, W, C, V, F)
     dom = max((k for k in kern_us if k in kbytes), key=lambda k: kern_us[k])
     achieved = kbytes[dom] / (kern_us[dom] * 1e-6) / 1e9
@@ -216,6 +279,117 @@ def main():
     if traffic is not None:
         roofline["traffic_frac"] = round(traffic / (kern_us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
 
+    legs = {}
+    # ---- leg: the public op surface (dirt_amd.rasterise_batch + torch.autograd), eager and graph-captured
+    if not args.no_api_leg:
+        import dirt_amd
+        bg_r, v_r, c_r = (t.clone().requires_grad_(True) for t in (bg, v, c))
+
+        def api_step():
+            px = dirt_amd.rasterise_batch(bg_r, v_r, c_r, f)
+            torch.autograd.grad(px, [bg_r, v_r, c_r], grad)
+
+        for _ in range(5):
+            api_step()
+        n_api = max(20, args.steps // 2)
+        t_eager = timed(api_step, n_api, barrier, world, device, shared)
+        g_api = graph_of(api_step, 1, cap_stream)
+        t_graph = timed(g_api.replay, n_api, barrier, world, device, shared)
+        legs["api_autograd"] = {
+            "what": "dirt_amd.rasterise_batch(...) + torch.autograd.grad per step (reference surface "
+                    "dirt/rasterise_ops.py:57-88), fresh outputs per call, cached scratch",
+            "eager_mpix_s": round(world * B * H * W * n_api / t_eager / 1e6, 1),
+            "eager_ms_per_step": round(t_eager * 1e3 / n_api, 4),
+            "graph_mpix_s": round(world * B * H * W * n_api / t_graph / 1e6, 1),
+            "graph_ms_per_step": round(t_graph * 1e3 / n_api, 4)}
+        del g_api
+
+    # ---- leg: rotating distinct frames, working set past the 256 MiB Infinity Cache (cold HBM)
+    if args.rotate > 1:
+        R = args.rotate
+        rot = []
+        for k in range(R):
+            hk, dk, gk, _ = make_inputs(cfg, rank + 1000 * (k + 1), device)
+            rot.append((RasteriseSession(B, H, W, C, V, F, device=device), dk, gk))
+        per_frame = sum(t.numel() * t.element_size() for t in rot[0][1]) + rot[0][2].numel() * 4
+        per_frame += sum(t.numel() * t.element_size() for t in (rot[0][0].pixels, rot[0][0].gbuffer, rot[0][0].saved,
+                                                             rot[0][0].grad_vertices, rot[0][0].grad_vertex_colors,
+                                                             rot[0][0].grad_background))
+        idx = [0]
+
+        def rot_step():
+            se, (bg_k, v_k, c_k, f_k), g_k = rot[idx[0] % R]
+            idx[0] += 1
+            se.forward(bg_k, v_k, c_k, f_k)
+            se.backward(g_k)
+
+        for _ in range(2 * R):
+            rot_step()
+        n_rot = max(R, (args.steps // R) * R)
+        g_rot = graph_of(lambda: [rot_step() for _ in range(R)], 1, cap_stream) if not args.no_graph else None
+        t_rot = timed((g_rot.replay if g_rot else lambda: [rot_step() for _ in range(R)]), n_rot // R, barrier,
+                      world, device, shared)
+        kr = kernel_times(rot_step, max(args.profile_steps // R, 1) * R)
+        legs["cold_cache"] = {
+            "what": "%d distinct frames rotated step by step (inputs, outputs and workspaces), %.0f MB touched per "
+                    "rotation > 256 MiB Infinity Cache" % (R, R * per_frame / 1e6),
+            "mpix_s": round(world * B * H * W * n_rot / t_rot / 1e6, 1),
+            "ms_per_step": round(t_rot * 1e3 / n_rot, 4),
+            "kernels_us": {k: round(u, 2) for k, u in kr.items()},
+            "grad_kernel_frac": round(kbytes["grad_kernel"] / (kr["grad_kernel"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        del g_rot, rot
+
+    # ---- leg (N > 1): the output all-gather over RCCL / xGMI, alone and overlapped with the next step
+    if world > 1 and not args.no_gather_leg:
+        from dirt_amd.sharding import gather_frames_async
+        batch = world * B
+        for _ in range(3):
+            gather_frames_async(sess.pixels, batch)[1]()
+        n_g = max(10, args.steps // 4)
+        t_g = timed(lambda: gather_frames_async(sess.pixels, batch)[1](), n_g, barrier, world, device, shared)
+        # pipelined: step k's frames move while step k+1 renders (two sessions, so a frame being gathered
+        # is never overwritten; the step that reuses a session first waits for its gather)
+        sess2 = RasteriseSession(B, H, W, C, V, F, device=device)
+        pair = (sess, sess2)
+        pend = [None, None]
+
+        def piped(k):
+            se = pair[k & 1]
+            if pend[k & 1] is not None:
+                pend[k & 1][0].wait()
+            se.forward(bg, v, c, f)
+            se.backward(grad)
+            pend[k & 1] = gather_frames_async(se.pixels, batch)
+
+        for k in range(4):
+            piped(k)
+        for p_ in pend:
+            p_[1]()
+        pend[:] = [None, None]
+        ctr = [0]
+
+        def piped_run():
+            piped(ctr[0])
+            ctr[0] += 1
+
+        def piped_all():
+            for _ in range(args.steps):
+                piped_run()
+            for p_ in pend:
+                if p_ is not None:
+                    p_[1]()
+
+        t_p = timed(piped_all, 1, barrier, world, device, shared)
+        recv = (world - 1) * B * H * W * C * 4
+        legs["gather"] = {
+            "what": "all_gather_into_tensor of every rank's pixels [%d,%d,%d,%d] over %s per step" %
+                    (B, H, W, C, "gloo (shared-GPU rehearsal)" if shared else "RCCL / xGMI"),
+            "gather_ms": round(t_g * 1e3 / n_g, 4),
+            "recv_bytes_per_rank": recv,
+            "recv_GBps_per_rank": round(recv / (t_g / n_g) / 1e9, 1),
+            "value_with_gather": round(world * B * H * W * args.steps / t_p / 1e6, 1),
+            "ms_per_step_with_gather": round(t_p * 1e3 / args.steps, 4)}
+
     cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref = cpu_baseline(host, grad_host, budget_s=args.cpu_budget)
@@ -232,12 +406,14 @@ def main():
             "config": {"workload": "%s: %d frame(s)/rank x %d random tris (r=%gpx), %dx%dx%d, fwd+bwd" %
                                    (args.config, B, F, _r, H, W, C),
                        "frames_per_rank": B, "height": H, "width": W, "channels": C, "faces": F, "vertices": V,
-                       "parallelism": "frames sharded over %d rank(s), no collective in step" % world,
+                       "parallelism": "frames sharded over %d rank(s); no collective in the step (the output "
+                                      "gather is measured as its own leg, legs.gather)" % world,
                        "hip_graph": not args.no_graph, "steps_per_graph": gs},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_vs_oracle": par,
             "kernels_us": {k: round(u, 2) for k, u in kern_us.items()},
+            "legs": legs,
         }
         print(json.dumps(out))
     if world > 1:

@@ -26,7 +26,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 BWD_ACCUMULATE = 1     # dirt_rasterise_bwd flags
@@ -42,6 +42,8 @@ SIGNATURES = {
     "dirt_workspace_sizes": (_I, [_I, _I, _I, _I, _I, _I, _I64, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "dirt_rasterise_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _U,
                                 _P, _P, _P]),
+    "dirt_rasterise_fwd_gbuffer": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _U,
+                                        _P, _P, _P, _P, _P, _P]),
     "dirt_hill_fwd": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _P]),
     "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _U, _P]),
     "dirt_scratch_clear": (_I, [_I, _I, _I, _I, _I64, _P, _SZ, _P]),

@@ -243,7 +243,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 6; }
+int dirt_abi_version(void) { return 7; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -267,10 +267,14 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
                               const int32_t *faces, const float *camera_pos, int B, int H, int W, int C, int V, int F,
                               int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes,
                               void *scratch, size_t scratch_bytes, int64_t bin_capacity, unsigned flags,
-                              float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream_)
+                              float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream_,
+                              GbufOut gbo = GbufOut{})
 {
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
+    const bool want_gb = gbo.depth || gbo.bary || gbo.face;
+    if (want_gb && shader_id != DIRT_SHADER_GOURAUD)
+        return fail(DIRT_EINVAL, "Rasterise: depth / barycentric / face outputs are produced by the Gouraud program only");
     if (shader_id < DIRT_SHADER_GOURAUD || shader_id > DIRT_SHADER_HILL)
         return fail(DIRT_EINVAL, "Rasterise: unsupported shader_id");
     if (shader_id != DIRT_SHADER_GOURAUD && !camera_pos)
@@ -324,6 +328,12 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
         LAUNCH_PROC(CC, DIRT_SHADER_HILL);                                                                       \
     else if (shader_id >= DIRT_SHADER_OCEANIC)                                                                   \
         LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC);                                                                    \
+    else if (want_gb)                                                                                            \
+        raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, true><<<grid, dim3(256), 0, stream>>>(                         \
+            background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
+            L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
+            zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo);          \
     else                                                                                                         \
     raster_kernel<CC><<<grid, dim3(256), 0, stream>>>(background, vertex_colors, recs, fdata, ccount, flag,       \
                                                       bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx),                     \
@@ -355,6 +365,19 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
     return rasterise_fwd_impl(background, C, vertices, vertex_colors, faces, camera_pos, B, H, W, C, V, F, shader_id,
                               pixels, gbuffer, saved, saved_bytes, scratch, scratch_bytes, bin_capacity, flags,
                               zero_grad_vertices, zero_grad_vertex_colors, stream_);
+}
+
+int dirt_rasterise_fwd_gbuffer(const float *background, const float *vertices, const float *vertex_colors,
+                               const int32_t *faces, int B, int H, int W, int C, int V, int F, float *pixels,
+                               int32_t *gbuffer, void *saved, size_t saved_bytes, void *scratch, size_t scratch_bytes,
+                               int64_t bin_capacity, unsigned flags, float *zero_grad_vertices,
+                               float *zero_grad_vertex_colors, float *depth, float *barycentrics, int32_t *face_ids,
+                               void *stream_)
+{
+    return rasterise_fwd_impl(background, C, vertices, vertex_colors, faces, nullptr, B, H, W, C, V, F,
+                              DIRT_SHADER_GOURAUD, pixels, gbuffer, saved, saved_bytes, scratch, scratch_bytes,
+                              bin_capacity, flags, zero_grad_vertices, zero_grad_vertex_colors, stream_,
+                              GbufOut{depth, barycentrics, face_ids});
 }
 
 int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *vertices, const int32_t *faces,

@@ -341,6 +341,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         for (int u = 0; u < 2; ++u) {
             const int k = t + 256 * u;
             if (k >= kHaloPix) continue;
+            // a background pixel with a non-finite value (G-buffers rendered over -inf,
+            // samples/deferred.py:67,81) defines no image difference: staged as "outside the frame", so
+            // none of its pairs carries vertex gradient; its grad_background stays G
+            if (gbv[u] == -1) {
+                bool fin = true;
+#pragma unroll
+                for (int c = 0; c < CM; ++c)
+                    if (c < C) fin = fin && __builtin_isfinite(Iv[u][c]);
+                gbv[u] = fin ? -1 : -2;
+            }
             s_gb[k] = gbv[u];
             s_cov[k] = (uint8_t)cvv[u];
             if (!ok[u]) continue;

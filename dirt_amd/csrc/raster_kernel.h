@@ -35,9 +35,11 @@ __device__ __forceinline__ int xcd_tile(int x, int n)
     return g * q + min(g, r) + k;
 }
 
-// Tiles per row with a host-computed reciprocal: tile / ntx = umulhi(tile, ceil(2^32 / ntx)), exact for
-// tile < 2^18 and ntx <= 2^9 (the error term tile * (m - 2^32/ntx) / 2^32 < 2^-14 never reaches the next
-// integer) -- two scalar instructions instead of a ~25-instruction division in every wave's prologue.
+// Tiles per row with a host-computed reciprocal: tile / ntx = umulhi(2 tile, m), m = ceil(2^31 / ntx).
+// m = 2^31/ntx + e/ntx with 0 <= e < ntx, so 2 tile m / 2^32 = tile/ntx + tile e / (ntx 2^31); the error
+// tile e / (ntx 2^31) < tile / 2^31 < 2^-13 (tile < 2^18) stays below the 1/ntx gap to the next integer
+// for ntx <= 512, so the floor is exact.  The 2^31 scale keeps m of ntx = 1 in 32 bits (2^32 / 1 would
+// not fit).  Two scalar instructions instead of a ~25-instruction division in every wave's prologue.
 struct TileGrid {
     int ntx;
     uint32_t inv;
@@ -367,7 +369,18 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
 #define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
                              // the procedural programs and the generic-C path keep their natural allocation)
 #endif
-template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD>
+// Optional deferred-shading outputs of the resolve (dirt_rasterise_fwd_gbuffer; instantiated only when
+// asked for, GB = true, so the default kernel is unchanged): window depth as the DEPTH24 buffer holds it,
+// read back as float (d / (2^24 - 1), 1.0 = cleared), perspective-correct barycentrics of the visible face's
+// three vertices, and the face index; every pointer may be null.  Upstream DIRT's G-buffer programs
+// (csrc/shaders.cpp:2187-2221) saved barycentrics, 1/gl_FragCoord.w and the face's vertex indices.
+struct GbufOut {
+    float *depth;         // [B,H,W]
+    float *bary;          // [B,H,W,3]
+    int32_t *face;        // [B,H,W], -1 background
+};
+
+template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
@@ -378,9 +391,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      float *__restrict__ zero_a,
                                                      int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
                                                      const float *__restrict__ verts, const float *__restrict__ cam,
-                                                     int sid, int tcb)
+                                                     int sid, int tcb, GbufOut gbo = GbufOut{})
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
+    static_assert(!(GB && kNoDepth), "hill has no depth buffer");
 #if defined(DIRT_RASTER_LDS_PAD) && DIRT_RASTER_LDS_PAD > 0
     __shared__ volatile char occupancy_probe[DIRT_RASTER_LDS_PAD];  // experiment: caps workgroups per CU
     if (threadIdx.x == 1023) occupancy_probe[0] = 0;
@@ -678,6 +692,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const int32_t best_rec = best != kKeyInit<kNoDepth> ? key_rec(key_low<kNoDepth>(best), F) : -1;
     if (best_rec < 0) {
         gbuffer[o] = -1;
+        if constexpr (GB) {
+            if (gbo.depth) gbo.depth[o] = 1.0f;
+            if (gbo.bary) {
+                gbo.bary[o * 3] = 0.0f;
+                gbo.bary[o * 3 + 1] = 0.0f;
+                gbo.bary[o * 3 + 2] = 0.0f;
+            }
+            if (gbo.face) gbo.face[o] = -1;
+        }
         if constexpr (SH == DIRT_SHADER_GOURAUD) covbits[o] = 0;
 #pragma unroll
         for (int c2 = 0; c2 < CM; ++c2)
@@ -705,6 +728,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         fE[0] = w.x; fE[1] = w.y; fE[2] = w.z;
     }
     parent_lambda_f(r, fE, fd.clipped == 0, lam);
+    if constexpr (GB) {
+        if (gbo.depth) gbo.depth[o] = (float)(uint32_t)(best >> 32) / 16777215.0f;
+        if (gbo.bary) {
+            gbo.bary[o * 3] = lam[0];
+            gbo.bary[o * 3 + 1] = lam[1];
+            gbo.bary[o * 3 + 2] = lam[2];
+        }
+        if (gbo.face) gbo.face[o] = face_of_record(best_rec, F);
+    }
     PHASE_TS(4);
     if constexpr (SH == DIRT_SHADER_OCEANIC_HORIZON) {
         // texCoordV = perspective-correct clip xy (shaders.cpp:19,21 alias texCoord to position); jitter by

@@ -382,7 +382,8 @@ void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int
 {
     ZeroFill zf{zero_a, zero_b, zero_a ? nzero_a : 0, zero_b ? nzero_b : 0, (F + kFacesPerBlock - 1) / kFacesPerBlock};
     // filler workgroups per frame row: ~16 float4 stores per thread, at most 64 in all
-    const int64_t z4 = (zf.na + zf.nb) / 4, want = std::min<int64_t>((z4 + 4095) / 4096, 64);
+    // (rounded up: a few accumulator floats in all, fewer than one float4, still need a filler workgroup)
+    const int64_t z4 = (zf.na + zf.nb + 3) / 4, want = std::min<int64_t>((z4 + 4095) / 4096, 64);
     const int nzb = z4 > 0 ? (int)std::max<int64_t>(1, (want + B - 1) / B) : 0;
     const dim3 grid((unsigned)(zf.nfb + nzb), (unsigned)B);
     setup_kernel<AB><<<grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse,

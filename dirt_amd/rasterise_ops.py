@@ -17,13 +17,17 @@ Differences from the reference, all deliberate:
   * errors are exceptions, never process aborts (csrc/rasterise_egl.cpp:85-503 LOG(FATAL)).
 There is no CPU path: the op requires a HIP device and raises if the native library is missing.
 """
+import collections
+import os
+import threading
+
 import numpy as np
 import torch
 
 from . import _lib
 
 __all__ = [
-    "rasterise", "rasterise_batch", "rasterise_grad",
+    "rasterise", "rasterise_batch", "rasterise_grad", "rasterise_gbuffer", "rasterise_batch_gbuffer", "GBuffer",
     "oceanic_no_cloud", "oceanic_simple_proxy", "oceanic_still_cloud", "oceanic_opt_flow", "hill",
 ]
 
@@ -43,12 +47,64 @@ def _as_tensor(x, dtype, device):
     return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
 
 
+class _Workspace:
+    """Per-(device, stream, layout) cache of the forward-only scratch (tile bins, bin counters).
+
+    A scratch zero-filled once stays clean across forwards of the same layout (the bin counters alternate
+    between two sets, include/dirt_mi355x.h DIRT_FWD_SCRATCH_CLEAN), so a cached one saves every call the
+    counter memset (128 MiB for B = 64 at 8192^2 with one 256-B line per counter) and the allocation.
+    Keyed by the stream too: two streams never share a scratch.  A few layouts are kept (LRU)."""
+
+    def __init__(self, keep=4):
+        self.keep = keep
+        self._lock = threading.Lock()
+        self._d = collections.OrderedDict()
+
+    def scratch(self, dev, stream, layout, nbytes):
+        key = (dev, stream, layout)
+        with self._lock:
+            t = self._d.get(key)
+            if t is not None:
+                self._d.move_to_end(key)
+                return t
+        # only the bin counters need zeroing (dirt_scratch_clear: a memset of the counter lines); the slabs
+        # are written before they are read
+        t = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+        B, H, W, F, cap = layout
+        _lib.check(_lib.load().dirt_scratch_clear(B, H, W, F, cap, t.data_ptr(), nbytes, stream))
+        with self._lock:
+            self._d[key] = t
+            while len(self._d) > self.keep:
+                self._d.popitem(last=False)
+        return t
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+
+
+_workspace = _Workspace()
+
+
+def _check_faces_now(faces, B, V, F, stream):
+    """Opt-in range check of the face indices (a kernel and a host sync): raises IndexError like the
+    SURVEY 8b return code 2.  The reference reads out of bounds (csrc/rasterise_egl.cpp:309-336 checks
+    shapes only); the forward itself culls such faces."""
+    flag = torch.empty((256,), dtype=torch.uint8, device=faces.device)
+    _lib.check(_lib.load().dirt_check_faces(faces.data_ptr(), B, V, F, flag.data_ptr(), 256, stream))
+
+
 class _RasteriseFunction(torch.autograd.Function):
-    """Rasterise op (csrc/rasterise_egl.cpp:33-53) with its registered gradient."""
+    """Rasterise op (csrc/rasterise_egl.cpp:33-53) with its registered gradient.
+
+    Outputs: pixels, the int32 record g-buffer and, when `want_gbuf`, depth / barycentrics / face ids
+    (non-differentiable).  When a gradient will be needed, the forward zero-fills the vertex and colour
+    gradient buffers in passing (filler workgroups of its setup launch) and the backward adds into them
+    (DIRT_BWD_ACCUMULATE), so a fwd+bwd costs no separate clearing launch."""
 
     @staticmethod
     def forward(ctx, background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
-                bin_capacity):
+                bin_capacity, want_gbuf, check_faces):
         B, V, F = vertices.shape[0], vertices.shape[1], faces.shape[1]
         H, W, C = height, width, channels
         dev = vertices.device
@@ -57,31 +113,60 @@ class _RasteriseFunction(torch.autograd.Function):
         pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
         saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
-        scratch = torch.empty((max(scratch_bytes, 1),), dtype=torch.uint8, device=dev)
+        need_grad = shader_id == _lib.SHADER_GOURAUD and any(ctx.needs_input_grad[:3]) and V > 0
+        gv = torch.empty((B, V, 4), dtype=torch.float32, device=dev) if need_grad else None
+        gc = torch.empty((B, V, C), dtype=torch.float32, device=dev) if need_grad else None
+        extra = ()
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
+            if check_faces:
+                _check_faces_now(faces, B, V, F, stream)
+            scratch = _workspace.scratch(dev, stream, (B, H, W, F, bin_capacity), scratch_bytes)
             cam = camera_pos.data_ptr() if camera_pos is not None else None
-            _lib.check(lib.dirt_rasterise_fwd(
-                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
-                B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
-                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, 0, None, None,
-                stream))
+            zg = (gv.data_ptr(), gc.data_ptr()) if need_grad else (None, None)
+            if want_gbuf:
+                depth = torch.empty((B, H, W), dtype=torch.float32, device=dev)
+                bary = torch.empty((B, H, W, 3), dtype=torch.float32, device=dev)
+                face_ids = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+                _lib.check(lib.dirt_rasterise_fwd_gbuffer(
+                    background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
+                    B, H, W, C, V, F, pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(), saved_bytes,
+                    scratch.data_ptr(), scratch_bytes, bin_capacity, _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1],
+                    depth.data_ptr(), bary.data_ptr(), face_ids.data_ptr(), stream))
+                extra = (depth, bary, face_ids)
+            else:
+                _lib.check(lib.dirt_rasterise_fwd(
+                    background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
+                    B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
+                    saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
+                    _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1], stream))
         ctx.save_for_backward(vertices, vertex_colors, faces, pixels, gbuffer, saved)
         ctx.dims = (B, H, W, C, V, F)
         ctx.shader_id = shader_id
-        ctx.mark_non_differentiable(gbuffer)
-        return pixels, gbuffer
+        ctx.prezeroed = (gv, gc) if need_grad else None
+        ctx.mark_non_differentiable(gbuffer, *extra)
+        return (pixels, gbuffer) + extra
 
     @staticmethod
-    def backward(ctx, grad_pixels, _grad_gbuffer):
+    def backward(ctx, grad_pixels, _grad_gbuffer, *_grad_extra):
         if ctx.shader_id != _lib.SHADER_GOURAUD:
             raise RuntimeError("only the Gouraud fragment program has a gradient (the reference registers none)")
         vertices, vertex_colors, faces, pixels, gbuffer, saved = ctx.saved_tensors
         B, H, W, C, V, F = ctx.dims
         dev = vertices.device
+        if grad_pixels is None:
+            grad_pixels = torch.zeros((B, H, W, C), dtype=torch.float32, device=dev)
         grad_pixels = grad_pixels.to(dtype=torch.float32).contiguous()
-        grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
-        grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
+        # the forward's zero-filled buffers serve one backward (autograd may keep the returned tensors as
+        # .grad); a second backward of the same graph (retain_graph) starts from fresh ones
+        flags = 0
+        if ctx.prezeroed is not None:
+            grad_vertices, grad_colors = ctx.prezeroed
+            ctx.prezeroed = None
+            flags = _lib.BWD_ACCUMULATE
+        else:
+            grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
+            grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
         grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         lib = _lib.load()
         with torch.cuda.device(dev):
@@ -90,8 +175,8 @@ class _RasteriseFunction(torch.autograd.Function):
                 vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), pixels.data_ptr(),
                 grad_pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(),
                 B, H, W, C, V, F, grad_vertices.data_ptr(), grad_colors.data_ptr(), grad_background.data_ptr(),
-                0, stream))
-        return grad_background, grad_vertices, grad_colors, None, None, None, None, None, None, None
+                flags, stream))
+        return (grad_background, grad_vertices, grad_colors) + (None,) * 9
 
 
 def _check_shapes(background, vertices, vertex_colors, faces, H, W, C):
@@ -123,10 +208,18 @@ _CAMERA_FLOATS = {
 
 def _upstream_positional(camera_pos, height, width, channels, name):
     """Upstream DIRT has no camera_pos: `rasterise(bg, v, c, f, H, W, C)` binds H to our camera_pos slot.
-    An integer there (a camera position is a float tensor / sequence, never a Python int) is that height;
-    shift height / width / channels / name back into place."""
+    An integer there (a camera position is a float tensor / sequence, never a Python int) is that height.
+
+    Upstream slot j (height, width, channels, name) lands in our slot j when passed positionally and in
+    our slot j+1 when passed by keyword.  The k positional values fill our first k slots and keyword
+    values only upstream slots >= k, i.e. our slots >= k+1, so our slot k is the first empty one: that
+    recovers k for fully positional, fully keyword and mixed calls such as
+    `rasterise_batch(bg, v, c, f, 48, width=64, channels=3)` or `(bg, v, c, f, 48, 64, channels=3)`."""
     if isinstance(camera_pos, (int, np.integer)) and not isinstance(camera_pos, bool):
-        return None, int(camera_pos), height, width, channels
+        ours = [int(camera_pos), height, width, channels, name]
+        k = next((i for i, x in enumerate(ours) if x is None), len(ours))
+        up = [ours[j] if j < k else ours[j + 1] for j in range(4)]
+        return (None,) + tuple(up)
     return camera_pos, height, width, channels, name
 
 
@@ -144,8 +237,12 @@ def _camera(camera_pos, shader_id, dev):
     return camera_pos
 
 
+# DIRT_CHECK_FACES=1: every call range-checks its face indices (one kernel + a host sync; off by default)
+_CHECK_FACES_DEFAULT = os.environ.get("DIRT_CHECK_FACES", "") not in ("", "0")
+
+
 def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
-                       bin_capacity=0, return_gbuffer=False):
+                       bin_capacity=0, return_gbuffer=False, want_gbuf=False, check_faces=None):
     dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
     background = _as_tensor(background, torch.float32, dev).contiguous()
     vertices = _as_tensor(vertices, torch.float32, dev).contiguous()
@@ -153,8 +250,13 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
     faces = _as_tensor(faces, torch.int32, dev).contiguous()
     camera_pos = _camera(camera_pos, shader_id, dev)
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
-    pixels, gbuffer = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos,
-                                               int(height), int(width), int(channels), shader_id, int(bin_capacity))
+    if check_faces is None:
+        check_faces = _CHECK_FACES_DEFAULT
+    outs = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos, int(height), int(width),
+                                    int(channels), shader_id, int(bin_capacity), bool(want_gbuf), bool(check_faces))
+    if want_gbuf:
+        return outs
+    pixels, gbuffer = outs
     return (pixels, gbuffer) if return_gbuffer else pixels
 
 
@@ -174,7 +276,7 @@ def _shader_id(shader):
 
 
 def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None, channels=None,
-              name=None, shader=None):
+              name=None, shader=None, check_faces=None):
     """Rasterises the given `vertices` and `faces` over `background` (reference dirt/rasterise_ops.py:10-54).
 
     Args:
@@ -194,6 +296,9 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
             registers none).  'oceanic', 'oceanic_still_cloud', 'oceanic_no_cloud',
             'oceanic_simple_proxy', 'oceanic_opt_flow': the programs of the reference's other procedural
             ops (same as calling those ops); forward only
+        check_faces: True raises IndexError if a face index lies outside [0, vertex count) (one extra
+            kernel and a host sync; default: the DIRT_CHECK_FACES environment variable, else off -- the
+            reference does not check and reads out of bounds, this op culls such faces)
 
     Returns:
         float32 [height, width, channels] pixels, differentiable w.r.t. background, vertices, vertex_colors.
@@ -213,11 +318,11 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
     vertex_colors = _as_tensor(vertex_colors, torch.float32, dev)
     faces = _as_tensor(faces, torch.int32, dev)
     return _rasterise_batched(background[None], vertices[None], vertex_colors[None], faces[None], camera_pos,
-                              height, width, channels, _shader_id(shader))[0]
+                              height, width, channels, _shader_id(shader), check_faces=check_faces)[0]
 
 
 def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
-                    channels=None, name=None, shader=None):
+                    channels=None, name=None, shader=None, check_faces=None):
     """Rasterises a batch of meshes with equal vertex and face counts (reference dirt/rasterise_ops.py:57-88).
 
     Conceptually `torch.stack([rasterise(bg_i, v_i, c_i, f_i) for ...])`; every argument carries a leading
@@ -233,7 +338,47 @@ def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None,
     if channels is None:
         channels = int(bshape[3])
     return _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels,
-                              _shader_id(shader))
+                              _shader_id(shader), check_faces=check_faces)
+
+
+GBuffer = collections.namedtuple("GBuffer", ["pixels", "depth", "barycentrics", "face_ids"])
+
+
+def rasterise_batch_gbuffer(background, vertices, vertex_colors, faces, height=None, width=None, channels=None,
+                            name=None, check_faces=None):
+    """`rasterise_batch` (Gouraud) that also returns the deferred-shading G-buffer of the same raster pass.
+
+    Returns GBuffer(pixels [B,H,W,C] (differentiable, as rasterise_batch), depth [B,H,W] (the DEPTH24 value
+    as float, 1.0 uncovered), barycentrics [B,H,W,3] (perspective-correct, of the visible face's vertices
+    faces[b, face_ids]; 0 uncovered), face_ids [B,H,W] int32 (-1 uncovered)).  Upstream DIRT rendered
+    these with separate G-buffer programs (csrc/shaders.cpp:2187-2221); here they come from the one
+    resolve (include/dirt_mi355x.h dirt_rasterise_fwd_gbuffer)."""
+    del name
+    bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
+    height = int(bshape[1]) if height is None else height
+    width = int(bshape[2]) if width is None else width
+    channels = int(bshape[3]) if channels is None else channels
+    px, _gb, depth, bary, face = _rasterise_batched(background, vertices, vertex_colors, faces, None, height, width,
+                                                    channels, _lib.SHADER_GOURAUD, want_gbuf=True,
+                                                    check_faces=check_faces)
+    return GBuffer(px, depth, bary, face)
+
+
+def rasterise_gbuffer(background, vertices, vertex_colors, faces, height=None, width=None, channels=None, name=None,
+                      check_faces=None):
+    """Single-frame `rasterise_batch_gbuffer` (shapes without the leading batch dimension)."""
+    del name
+    bshape = tuple(background.shape) if hasattr(background, "shape") else np.shape(background)
+    height = int(bshape[0]) if height is None else height
+    width = int(bshape[1]) if width is None else width
+    channels = int(bshape[2]) if channels is None else channels
+    dev = _device_of(background, vertices, vertex_colors, faces)
+    g = rasterise_batch_gbuffer(_as_tensor(background, torch.float32, dev)[None],
+                                _as_tensor(vertices, torch.float32, dev)[None],
+                                _as_tensor(vertex_colors, torch.float32, dev)[None],
+                                _as_tensor(faces, torch.int32, dev)[None], height, width, channels,
+                                check_faces=check_faces)
+    return GBuffer(*(t[0] for t in g))
 
 
 def _procedural_op(opname, shader, ref):

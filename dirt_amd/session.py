@@ -38,7 +38,10 @@ class RasteriseSession:
         self.grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         self._lib = _lib.load()
         self._inputs = None
-        self.scratch.zero_()  # clean once; every forward leaves it clean
+        # clean once (the bin counters; the slabs are written before they are read); every forward leaves
+        # it clean
+        _lib.check(self._lib.dirt_scratch_clear(B, H, W, F, self.bin_capacity, self.scratch.data_ptr(),
+                                                self.scratch_bytes, torch.cuda.current_stream(dev).cuda_stream))
 
     def _check(self, t, shape, dtype):
         if t.device != self.device or t.dtype != dtype or tuple(t.shape) != shape or not t.is_contiguous():

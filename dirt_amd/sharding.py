@@ -36,6 +36,55 @@ def gather_frames(local, batch, group=None):
     return torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
 
 
+def gather_frames_async(local, batch, group=None):
+    """Start gathering per-rank frame blocks; returns (work, finish) where finish() -> the full batch.
+
+    The collective runs on the backend's own stream (RCCL: its NCCL stream, which waits for the work
+    already queued on the current stream), so the caller can queue the next step's render while the
+    frames move over xGMI; work.wait() makes the current stream wait for the gather."""
+    world = dist.get_world_size(group)
+    sizes = [shard_bounds(batch, r, world) for r in range(world)]
+    mx = max(hi - lo for lo, hi in sizes)
+    if local.shape[0] == mx:
+        pad = local.contiguous()
+    else:
+        pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[: local.shape[0]] = local
+    out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    work = dist.all_gather_into_tensor(out, pad, group=group, async_op=True)
+
+    def finish():
+        work.wait()
+        if all(hi - lo == mx for lo, hi in sizes):
+            return out
+        return torch.cat([out[r * mx: r * mx + hi - lo] for r, (lo, hi) in enumerate(sizes)], 0)
+
+    return work, finish
+
+
+class _SharedGradAllReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, grad):
+        grad = grad.contiguous().clone()
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=ctx.group)
+        return grad, None
+
+
+def shared_across_ranks(x, group=None):
+    """Mark a tensor that every rank's frames use (e.g. one mesh's vertices tiled over the batch,
+    tests/rasterise_tests.py:89): identity forward; in the backward its gradient is summed over the ranks
+    (one all-reduce: RCCL over xGMI with the "nccl" backend), so every rank ends up with the
+    gradient of the whole batch, as if one process had rendered every frame.  ~16 V bytes per step."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return x
+    return _SharedGradAllReduce.apply(x, group)
+
+
 def rasterise_batch_sharded(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
                             channels=None, group=None, gather=False, render=rasterise_batch):
     """rasterise_batch over this rank's contiguous share of the frames.
@@ -50,7 +99,9 @@ def rasterise_batch_sharded(background, vertices, vertex_colors, faces, camera_p
     lo, hi = shard_bounds(B, rank, world)
     local = render(background[lo:hi], vertices[lo:hi], vertex_colors[lo:hi], faces[lo:hi], camera_pos=camera_pos,
                    height=height, width=width, channels=channels)
-    if not gather or world == 1:
+    if not gather:
         return local, (lo, hi)
+    if world == 1:
+        return local.detach()
     with torch.no_grad():
         return gather_frames(local.detach(), B, group=group)

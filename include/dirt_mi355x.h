@@ -68,7 +68,7 @@ extern "C" {
 
 /* ABI version, bumped on any signature or workspace-layout change (4: + dirt_hill_fwd, shader ids 6 and 7;
  * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
- * separate 256-B lines of the scratch) */
+ * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -93,6 +93,21 @@ int dirt_rasterise_fwd(const float *background, const float *vertices, const flo
                        void *saved, size_t saved_bytes, void *scratch, size_t scratch_bytes,
                        int64_t bin_capacity, unsigned flags,
                        float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream);
+/* Forward with the deferred-shading G-buffer (Gouraud program): dirt_rasterise_fwd plus, per pixel,
+ *   depth        [B,H,W]   window depth as the reference's DEPTH24 buffer holds it (rasterise_egl.cpp:248),
+ *                          read back as float: d / (2^24 - 1); 1.0 (the clear value, :449) where uncovered
+ *   barycentrics [B,H,W,3] perspective-correct barycentrics of the visible face's vertices
+ *                          faces[b, face_ids, 0..2] (the `smooth` interpolation, shaders.cpp:16-34); 0 uncovered
+ *   face_ids     [B,H,W]   index of the visible face, -1 uncovered
+ * (rows top first, like pixels).  Each may be NULL.  Replaces upstream DIRT's G-buffer programs
+ * backward_vertex / backward_fragment (csrc/shaders.cpp:2187-2221: barycentrics, 1/gl_FragCoord.w and the
+ * face's vertex indices) and the Vertex layout of csrc/rasterise_grad_common.h:5-11. */
+int dirt_rasterise_fwd_gbuffer(const float *background, const float *vertices, const float *vertex_colors,
+                               const int32_t *faces, int B, int H, int W, int C, int V, int F,
+                               float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes,
+                               void *scratch, size_t scratch_bytes, int64_t bin_capacity, unsigned flags,
+                               float *zero_grad_vertices, float *zero_grad_vertex_colors,
+                               float *depth, float *barycentrics, int32_t *face_ids, void *stream);
 /* Forward of the Hill op (csrc/hill.cpp:282-498, REGISTER_OP("Hill") :33-53): DIRT_SHADER_HILL with a
  * terrain lookup `terrain` [B,H,W,terrain_channels] (1, 3 or 4 channels, uploaded like a background,
  * rasterise_egl.cu:33-47) in place of the background; vertex colours are not read.  pixels [B,H,W,C];

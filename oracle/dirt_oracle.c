@@ -1127,21 +1127,23 @@ void oracle_hill_pixel(const float *tex_frame, int H, int W, int Ct, float tx, f
 
 static int fwd_core(const float *background, int Cb, const float *vertices, const float *vertex_colors,
                     const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
-                    const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads);
+                    const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads,
+                    float *depth, float *bary, int32_t *face_ids);
 
 int oracle_rasterise_fwd_shader(const float *background, const float *vertices, const float *vertex_colors,
                                 const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
                                 const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
 {
     return fwd_core(background, C, vertices, vertex_colors, faces, B, H, W, C, V, F, shader_id, camera_pos, pixels,
-                    gbuffer, nthreads);
+                    gbuffer, nthreads, NULL, NULL, NULL);
 }
 
 /* the Hill op (csrc/hill.cpp): terrain lookup [B,H,W,Ct] (Ct in {1,3,4}) in place of the background */
 int oracle_hill_fwd(const float *terrain, int Ct, const float *vertices, const int32_t *faces, int B, int H, int W,
                     int C, int V, int F, const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
 {
-    return fwd_core(terrain, Ct, vertices, NULL, faces, B, H, W, C, V, F, 7, camera_pos, pixels, gbuffer, nthreads);
+    return fwd_core(terrain, Ct, vertices, NULL, faces, B, H, W, C, V, F, 7, camera_pos, pixels, gbuffer, nthreads,
+                    NULL, NULL, NULL);
 }
 
 int oracle_rasterise_fwd(const float *background, const float *vertices, const float *vertex_colors,
@@ -1152,13 +1154,26 @@ int oracle_rasterise_fwd(const float *background, const float *vertices, const f
                                        pixels, gbuffer, nthreads);
 }
 
+/* Gouraud forward plus the deferred-shading G-buffer of dirt_rasterise_fwd_gbuffer (include/dirt_mi355x.h):
+ * depth = the DEPTH24 value read back as float, d / (2^24 - 1) (1.0 uncovered, the clear value,
+ * csrc/rasterise_egl.cpp:248,449); barycentrics = the R6 perspective-correct lambdas of the visible face's
+ * vertices (0 uncovered); face_ids = the visible face (-1 uncovered).  Each output may be NULL. */
+int oracle_rasterise_fwd_gbuffer(const float *background, const float *vertices, const float *vertex_colors,
+                                 const int32_t *faces, int B, int H, int W, int C, int V, int F, float *pixels,
+                                 int32_t *gbuffer, float *depth, float *bary, int32_t *face_ids, int nthreads)
+{
+    return fwd_core(background, C, vertices, vertex_colors, faces, B, H, W, C, V, F, 0, NULL, pixels, gbuffer,
+                    nthreads, depth, bary, face_ids);
+}
+
 /* shader_id (include/dirt_mi355x.h): 0 Gouraud, 1 oceanic_horizon, 2..5 the oceanic family,
  * 6 oceanic_opt_flow, 7 hill (no depth test: the last face in draw order wins, hill.cpp:194;
  * uncovered pixels 0, hill never writes its colour attachment there); camera_pos: host floats.
  * background has Cb channels (Cb == C except for hill's terrain lookup). */
 static int fwd_core(const float *background, int Cb, const float *vertices, const float *vertex_colors,
                     const int32_t *faces, int B, int H, int W, int C, int V, int F, int shader_id,
-                    const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads)
+                    const float *camera_pos, float *pixels, int32_t *gbuffer, int nthreads,
+                    float *depth, float *bary, int32_t *face_ids)
 {
     int status = 0;
 #ifdef _OPENMP
@@ -1218,6 +1233,9 @@ static int fwd_core(const float *background, int Cb, const float *vertices, cons
                     if (gbuffer) gbuffer[o] = ri < 0 ? -1 : (ri | (clipped[recs[ri].face] ? GBUF_MULTI : 0));
                     if (ri < 0) {
                         for (int c = 0; c < C; ++c) out[c] = shader_id == 7 ? 0.0f : bg[c];
+                        if (depth) depth[o] = 1.0f;
+                        if (bary) bary[o * 3] = bary[o * 3 + 1] = bary[o * 3 + 2] = 0.0f;
+                        if (face_ids) face_ids[o] = -1;
                         continue;
                     }
                     const orc_rec *r = &recs[ri];
@@ -1225,6 +1243,9 @@ static int fwd_core(const float *background, int Cb, const float *vertices, cons
                     edge_values(r, i, j, E);
                     float lam[3] = {0.0f, 0.0f, 0.0f};
                     parent_lambda(r, E, lam);
+                    if (depth) depth[o] = (float)(uint32_t)(keys[p] >> 32) / 16777215.0f;
+                    if (bary) { bary[o * 3] = lam[0]; bary[o * 3 + 1] = lam[1]; bary[o * 3 + 2] = lam[2]; }
+                    if (face_ids) face_ids[o] = r->face;
                     const int32_t *f3 = fb + 3 * (int64_t)r->face;
                     if (shader_id == 6 || shader_id == 7) {
                         const float tx = (lam[0] * vb[(int64_t)f3[0] * 4] + lam[1] * vb[(int64_t)f3[1] * 4]) +
@@ -1319,6 +1340,13 @@ static void add_pair_owner(const orc_rec *r, const float *vb, const int32_t *fb,
     }
 }
 
+static int all_finite(const float *x, int C)
+{
+    for (int c = 0; c < C; ++c)
+        if (!isfinite(x[c])) return 0;
+    return 1;
+}
+
 int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces,
                          const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
                          int B, int H, int W, int C, int V, int F,
@@ -1357,6 +1385,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
                     int64_t o = ((int64_t)b * H + row) * W + i;
                     const float *G = grad_pixels + o * C, *I = pixels + o * C;
                     int32_t rp = gbuffer[o] < 0 ? -1 : (gbuffer[o] & GBUF_INDEX_MASK);
+                    const int undef_p = rp < 0 && !all_finite(I, C);
                     float *gbg = grad_background + o * C;
                     if (rp < 0) {
                         for (int c = 0; c < C; ++c) gbg[c] = G[c];
@@ -1379,6 +1408,10 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
                         int32_t rq = gbuffer[o2] < 0 ? -1 : (gbuffer[o2] & GBUF_INDEX_MASK);
                         if (rp < 0 && rq < 0) continue;
                         const float *G2 = grad_pixels + o2 * C, *I2 = pixels + o2 * C;
+                        /* a background pixel with a non-finite value (samples/deferred.py:67,81 renders
+                         * G-buffers over -inf) defines no image difference: its pairs carry no vertex
+                         * gradient */
+                        if (undef_p || (rq < 0 && !all_finite(I2, C))) continue;
                         float acc = 0.0f;
                         for (int c = 0; c < C; ++c) acc += (G[c] + G2[c]) * (I2[c] - I[c]);
                         float s = -0.5f * acc;

@@ -30,6 +30,8 @@ def load():
         lib.oracle_rasterise_fwd.restype = I
         lib.oracle_rasterise_fwd_shader.argtypes = [P, P, P, P, I, I, I, I, I, I, I, P, P, P, I]
         lib.oracle_rasterise_fwd_shader.restype = I
+        lib.oracle_rasterise_fwd_gbuffer.argtypes = [P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I]
+        lib.oracle_rasterise_fwd_gbuffer.restype = I
         lib.oracle_oceanic_horizon_pixel.argtypes = [P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
         lib.oracle_oceanic_horizon_pixel.restype = None
         lib.oracle_oceanic_family_pixel.argtypes = [I, P, I, I, I, ctypes.c_float, ctypes.c_float, P, P]
@@ -123,6 +125,24 @@ def rasterise_fwd(background, vertices, vertex_colors, faces, nthreads=0, shader
     st = load().oracle_rasterise_fwd_shader(_ptr(bg), _ptr(vs), _ptr(cs), _ptr(fs), B, H, W, C, V, F, shader_id,
                                             _ptr(cam), _ptr(pixels), _ptr(gbuf), nthreads)
     return pixels, gbuf, st
+
+
+def rasterise_fwd_gbuffer(background, vertices, vertex_colors, faces, nthreads=0):
+    """Gouraud forward plus the deferred-shading G-buffer (dirt_rasterise_fwd_gbuffer).
+
+    Returns (pixels [B,H,W,C], gbuffer [B,H,W], depth [B,H,W] float32, barycentrics [B,H,W,3] float32,
+    face_ids [B,H,W] int32, status)."""
+    bg, vs, cs, fs = _f32(background), _f32(vertices), _f32(vertex_colors), _i32(faces)
+    B, H, W, C = bg.shape
+    V, F = vs.shape[1], fs.shape[1]
+    pixels = np.empty((B, H, W, C), np.float32)
+    gbuf = np.empty((B, H, W), np.int32)
+    depth = np.empty((B, H, W), np.float32)
+    bary = np.empty((B, H, W, 3), np.float32)
+    face = np.empty((B, H, W), np.int32)
+    st = load().oracle_rasterise_fwd_gbuffer(_ptr(bg), _ptr(vs), _ptr(cs), _ptr(fs), B, H, W, C, V, F, _ptr(pixels),
+                                             _ptr(gbuf), _ptr(depth), _ptr(bary), _ptr(face), nthreads)
+    return pixels, gbuf, depth, bary, face, st
 
 
 def oceanic_horizon_pixel(background_frame, tx, ty, camera_pos):

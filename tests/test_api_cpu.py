@@ -14,9 +14,10 @@ def test_op_names_and_signatures_match_the_reference():
     # dirt/rasterise_ops.py:10,57,91,110,129,148,167,186 (camera_pos made optional)
     for name in ("rasterise", "rasterise_batch"):
         params = list(inspect.signature(getattr(dirt_amd, name)).parameters)
-        # the reference's parameters in its order; `shader` is an added keyword (fork's fragment program)
+        # the reference's parameters in its order; `shader` (fork's fragment program) and `check_faces`
+        # (opt-in index check) are added keywords after them
         assert params == ["background", "vertices", "vertex_colors", "faces", "camera_pos", "height", "width",
-                          "channels", "name", "shader"]
+                          "channels", "name", "shader", "check_faces"]
         sig = inspect.signature(getattr(dirt_amd, name))
         assert all(sig.parameters[p].default is None for p in params[4:])
     for name in ("rasterise_grad", "oceanic_no_cloud", "oceanic_simple_proxy", "oceanic_still_cloud",
@@ -114,6 +115,11 @@ def test_upstream_positional_call_form():
     cam = [0.0] * 8
     assert up(cam, 48, 64, 3, None) == (cam, 48, 64, 3, None)
     assert up(None, None, None, None, None) == (None, None, None, None, None)
+    # mixed positional / keyword forms: keywords stay in their slots
+    assert up(48, None, 64, 3, None) == (None, 48, 64, 3, None)      # (.., 48, width=64, channels=3)
+    assert up(48, 64, None, 3, None) == (None, 48, 64, 3, None)      # (.., 48, 64, channels=3)
+    assert up(48, None, None, 3, "nm") == (None, 48, None, 3, "nm")  # (.., 48, channels=3, name="nm")
+    assert up(48, None, None, None, None) == (None, 48, None, None, None)
     if not torch.cuda.is_available():
         # the positional upstream call reaches the device check, not a camera_pos error
         bg = np.zeros((1, 8, 8, 3), np.float32)

@@ -161,3 +161,51 @@ def test_oracle_empty_and_degenerate_inputs():
     px, gb, st = oracle.rasterise_fwd(bg[None], v[None], c[None], f2[None])
     assert st == 2  # out-of-range index reported, face culled
     assert not np.isin(gb[0] & ((1 << 30) - 1), [0, 1]).any()
+
+
+@pytest.mark.parametrize("fill", [float("-inf"), float("nan")])
+def test_non_finite_background_rule(fill):
+    """a background pixel holding a non-finite value (samples/deferred.py:67,81 renders over
+    -inf) defines no image difference, so its pixel pairs carry no vertex gradient.  README square over
+    -inf with a constant colour: the silhouette pairs are the only ones with a non-zero difference, so the
+    vertex gradient is exactly 0 (over a finite background it is the translation / area KAT above)."""
+    bg, v, c, f = (a[None] for a in scenes.readme_square())
+    bg = np.full_like(bg, fill)
+    px, gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+    assert np.isnan(px[0, 0, 0, 0]) if np.isnan(fill) else px[0, 0, 0, 0] == fill
+    gv, gc, gbg = oracle.rasterise_bwd(v, c, f, px, np.ones_like(px), gb)
+    assert np.all(gv == 0.0)
+    # colour and background gradients do not depend on the background's values
+    px0, gb0, _ = oracle.rasterise_fwd(np.zeros_like(bg), v, c, f)
+    gv0, gc0, gbg0 = oracle.rasterise_bwd(v, c, f, px0, np.ones_like(px0), gb0)
+    np.testing.assert_array_equal(gc, gc0)
+    np.testing.assert_array_equal(gbg, gbg0)
+    # a random scene over a partly non-finite background: every gradient finite
+    bg, v, c, f = (a[None] for a in scenes.random_triangles(F=300, W=64, H=48, radius_px=8.0, seed=2))
+    bg = bg.copy()
+    bg[0, ::2, ::3, 0] = fill
+    px, gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+    g = np.random.default_rng(0).standard_normal(px.shape).astype(np.float32)
+    gv, gc, gbg = oracle.rasterise_bwd(v, c, f, px, g, gb)
+    assert np.all(np.isfinite(gv)) and np.all(np.isfinite(gc)) and np.abs(gv).max() > 0
+
+
+def test_gbuffer_outputs_consistent():
+    """oracle.rasterise_fwd_gbuffer (the checker of dirt_rasterise_fwd_gbuffer): depth is the DEPTH24 value
+    as float (1.0 uncovered), barycentrics interpolate the Gouraud pixels, face ids name the visible face."""
+    bg, v, c, f = scenes.random_triangles(F=400, W=80, H=64, radius_px=9.0, seed=4, perspective=True)
+    px, gb, depth, bary, face, st = oracle.rasterise_fwd_gbuffer(bg[None], v[None], c[None], f[None])
+    px2, gb2, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
+    np.testing.assert_array_equal(px, px2)
+    np.testing.assert_array_equal(gb, gb2)
+    cov = face[0] >= 0
+    assert np.array_equal(cov, gb[0] >= 0)
+    assert np.all(depth[0][~cov] == 1.0) and np.all(bary[0][~cov] == 0)
+    d24 = np.round(depth[0][cov].astype(np.float64) * (2 ** 24 - 1))
+    assert np.abs(d24 - depth[0][cov] * (2 ** 24 - 1)).max() < 2.0  # a 24-bit quantum
+    interp = np.einsum("nk,nkc->nc", bary[0][cov], c[f[face[0][cov]]])
+    np.testing.assert_allclose(interp, px[0][cov], rtol=1e-5, atol=1e-5)
+    # README square: z = 0 -> window depth 0.5, quantised
+    _, _, depth, _, face, _ = oracle.rasterise_fwd_gbuffer(*(a[None] for a in scenes.readme_square()))
+    assert set(np.unique(face)) == {-1, 0, 1}
+    assert np.all(depth[face >= 0] == np.float32(np.float32(8388608) / np.float32(16777215)))

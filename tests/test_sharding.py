@@ -14,7 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import scenes
-from dirt_amd.sharding import gather_frames, rasterise_batch_sharded, shard_bounds
+from dirt_amd.sharding import (gather_frames, gather_frames_async, rasterise_batch_sharded, shard_bounds,
+                               shared_across_ranks)
 from oracle import oracle
 
 
@@ -52,7 +53,13 @@ def _worker(rank, world, port, inputs, outq):
         local, (lo, hi) = rasterise_batch_sharded(bg, v, c, f, render=_oracle_render)
         full = gather_frames(local, bg.shape[0])
         full2 = rasterise_batch_sharded(bg, v, c, f, render=_oracle_render, gather=True)
-        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy()))
+        work, finish = gather_frames_async(local, bg.shape[0])
+        full3 = finish()
+        # a parameter shared by every rank's frames: its gradient is summed over the ranks
+        x = torch.arange(6, dtype=torch.float32).requires_grad_(True)
+        loss = (shared_across_ranks(x) * (rank + 1)).sum() + (x * x).sum() * 0.0
+        loss.backward()
+        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy(), full3.numpy(), x.grad.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -73,7 +80,9 @@ def test_two_rank_sharded_batch_matches_single_process(B):
         assert p.exitcode == 0
     res.sort(key=lambda r: r[0])
     covered = []
-    for rank, lo, hi, local, full, full2 in res:
+    for rank, lo, hi, local, full, full2, full3, xgrad in res:
+        np.testing.assert_array_equal(full3, ref)          # the async all_gather_into_tensor path
+        np.testing.assert_array_equal(xgrad, np.full(6, 3.0, np.float32))  # (1 + 2) summed over ranks
         assert (lo, hi) == shard_bounds(B, rank, 2)
         np.testing.assert_array_equal(local, ref[lo:hi])   # each rank renders only its frames
         np.testing.assert_array_equal(full, ref)           # all-gather reassembles the batch

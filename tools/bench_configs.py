@@ -1,5 +1,8 @@
 """Throughput of every BASELINE.json config on one GPU ("report all"): forward+backward steps
-through RasteriseSession replayed from HIP graphs (10 steps per graph), inputs resident in HBM.
+through RasteriseSession replayed from HIP graphs (10 steps per graph), inputs resident in HBM; beside
+each, the CPU oracle (test infrastructure, OpenMP on the job's host-core share) on the same frames
+(BASELINE.md section 2's CPU column), and for c4 the whole deferred-shading chain of samples/deferred.py
+(tests/deferred_pipeline.py) through the public op + autograd.
 
     python tools/bench_configs.py > profiles/r01/configs.jsonl
     python tools/bench_configs.py stress c5   # only the configs whose names contain these
@@ -27,6 +30,52 @@ CONFIGS = {
                                                   for b in range(8)],
     "c3_stress_r64_1024x1024x3": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, radius_px=64.0, seed=0)],
 }
+
+
+def cpu_oracle(host, g, budget_s=3.0):
+    """The CPU oracle's fwd+bwd on the same frames (median over repetitions within ~budget_s)."""
+    from oracle import oracle
+    import bench
+    n = bench.cpu_threads()
+    bg, v, c, f = host
+    ts = []
+    t_start = time.perf_counter()
+    while not ts or (time.perf_counter() - t_start < budget_s and len(ts) < 20):
+        t0 = time.perf_counter()
+        px, gb, _ = oracle.rasterise_fwd(bg, v, c, f, nthreads=n)
+        oracle.rasterise_bwd(v, c, f, px, g, gb, nthreads=n)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"cpu_Mpixels_per_s": round(bg.shape[0] * bg.shape[1] * bg.shape[2] / t / 1e6, 2), "cpu_threads": n,
+            "cpu_ms_per_step": round(t * 1e3, 2)}
+
+
+def deferred_chain(steps=20):
+    """c4 as the reference sample runs it: three 3-channel G-buffer renders + dilation + lighting + loss,
+    backward to world-space vertices (tests/deferred_pipeline.py), through dirt_amd.rasterise + autograd."""
+    import deferred_pipeline as dp
+    dev = torch.device("cuda", 0)
+    H = W = 512
+    world, faces, albedo = dp.grid_surface()
+    Vw = torch.from_numpy(world).to(dev).requires_grad_(True)
+    f = torch.from_numpy(faces).to(dev)
+    al = torch.from_numpy(albedo).to(dev)
+    wts = torch.rand((H, W, 3), device=dev)
+
+    def step():
+        L, _, _ = dp.chain(dp.hip_render, Vw, f, al, H, W, wts)
+        torch.autograd.grad(L, [Vw])
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"config": "c4_deferred_chain_3x512x512x3_grad_to_world_vertices", "faces": len(faces),
+            "ms_per_step_eager": round(dt * 1e3, 3), "Mpixels_per_s_fwd_bwd": round(H * W / dt / 1e6, 1)}
 
 
 def run(name, frames, steps=100):
@@ -61,9 +110,13 @@ def run(name, frames, steps=100):
     torch.cuda.synchronize()
     prof = _lib.profile_read()
     _lib.profile_enable(False)
-    return {"config": name, "frames": B, "H": H, "W": W, "C": C, "faces": F, "vertices": V,
-            "Mpixels_per_s_fwd_bwd": round(B * H * W / dt / 1e6, 1), "us_per_step": round(dt * 1e6, 2),
-            "kernels_us": {k: round(ms / n * 1e3, 2) for k, (n, ms) in prof.items() if n}}
+    out = {"config": name, "frames": B, "H": H, "W": W, "C": C, "faces": F, "vertices": V,
+           "Mpixels_per_s_fwd_bwd": round(B * H * W / dt / 1e6, 1), "us_per_step": round(dt * 1e6, 2),
+           "kernels_us": {k: round(ms / n * 1e3, 2) for k, (n, ms) in prof.items() if n}}
+    if os.environ.get("DIRT_NO_CPU") != "1":
+        out.update(cpu_oracle(host, g.cpu().numpy()))
+        out["gpu_over_cpu"] = round(out["Mpixels_per_s_fwd_bwd"] / max(out["cpu_Mpixels_per_s"], 1e-9), 1)
+    return out
 
 
 def main():
@@ -72,6 +125,8 @@ def main():
     for name, make in CONFIGS.items():
         if not sel or any(k in name for k in sel):
             print(json.dumps(run(name, make())), flush=True)
+    if not sel or any(k in "c4_deferred_chain" for k in sel):
+        print(json.dumps(deferred_chain()), flush=True)
 
 
 if __name__ == "__main__":
