@@ -22,7 +22,22 @@ ORACLE = oracle/libdirt_oracle.so
 HIP_SRC = dirt_amd/csrc/dirt_raster.hip
 HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/setup_kernel.h dirt_amd/csrc/raster_kernel.h dirt_amd/csrc/grad_kernel.h dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h
 
-all: $(LIB) $(ORACLE)
+# the public op's C++ autograd function (PyTorch extension over the C ABI; dirt_amd/csrc/torch_op.cpp)
+PY ?= python3
+TORCH_DIR := $(shell $(PY) -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
+PY_INC := $(shell $(PY) -c "import sysconfig; print(sysconfig.get_paths()['include'])" 2>/dev/null)
+EXT_SUFFIX := $(shell $(PY) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))" 2>/dev/null)
+CXX11ABI := $(shell $(PY) -c "import torch; print(int(torch._C._GLIBCXX_USE_CXX11_ABI))" 2>/dev/null)
+TORCH_EXT = dirt_amd/_dirt_torch$(EXT_SUFFIX)
+EXT_CXXFLAGS = -O2 -std=c++17 -fPIC -shared -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 \
+               -DTORCH_EXTENSION_NAME=_dirt_torch -DTORCH_API_INCLUDE_EXTENSION_H -D_GLIBCXX_USE_CXX11_ABI=$(CXX11ABI) \
+               -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include -I/opt/rocm/include -I$(PY_INC)
+EXT_LDFLAGS = -L$(TORCH_DIR)/lib -ltorch -ltorch_cpu -ltorch_python -lc10 -lc10_hip -Wl,-rpath,$(TORCH_DIR)/lib -ldl
+
+all: $(LIB) $(ORACLE) $(TORCH_EXT)
+
+$(TORCH_EXT): dirt_amd/csrc/torch_op.cpp include/dirt_mi355x.h
+	g++ $(EXT_CXXFLAGS) -o $@ $< $(EXT_LDFLAGS)
 
 $(LIB): $(HIP_DEPS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRC)
@@ -38,6 +53,6 @@ asm: $(HIP_DEPS)
 	mkdir -p build/asm && cd build/asm && $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o dirt_raster.s ../../$(HIP_SRC)
 
 clean:
-	rm -f $(LIB) $(ORACLE)
+	rm -f $(LIB) $(ORACLE) $(TORCH_EXT)
 
 .PHONY: all clean asm

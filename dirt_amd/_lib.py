@@ -5,6 +5,7 @@ This is the Python analogue of `tf.load_op_library(_lib_path + '/librasterise.so
 There is no fallback: if the library is missing or cannot be loaded the import of the op fails loudly.
 """
 import ctypes
+import functools
 import os
 
 _here = os.path.dirname(os.path.abspath(__file__))
@@ -92,6 +93,7 @@ def check(rc):
     raise DirtError(msg)
 
 
+@functools.lru_cache(maxsize=256)
 def workspace_sizes(B, H, W, C, V, F, bin_capacity=0):
     lib = load()
     saved = ctypes.c_size_t(0)

@@ -380,7 +380,13 @@ struct GbufOut {
     int32_t *face;        // [B,H,W], -1 background
 };
 
-template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false>
+// FUSED (frames of at most kFusedMaxF faces, Gouraud): no setup launch and no bins -- every workgroup sets up
+// all faces of its frame itself into LDS (one face per thread, clipping included) and filters them against
+// its tile (the overflow path's all-records filter, reading LDS); the workgroup of tile 0 writes the records
+// and FaceData of its frame to `saved` for the backward.  One launch instead of two for small scenes.
+constexpr int kFusedMaxF = 32;
+
+template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
@@ -391,10 +397,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      float *__restrict__ zero_a,
                                                      int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
                                                      const float *__restrict__ verts, const float *__restrict__ cam,
-                                                     int sid, int tcb, GbufOut gbo = GbufOut{})
+                                                     int sid, int tcb, GbufOut gbo = GbufOut{},
+                                                     const int32_t *__restrict__ faces = nullptr)
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     static_assert(!(GB && kNoDepth), "hill has no depth buffer");
+    static_assert(!FUSED || SH == DIRT_SHADER_GOURAUD, "the fused small-scene forward is Gouraud only");
+    // FUSED: the frame's records and FaceData, set up in LDS by this workgroup
+    __shared__ Rec s_recs[FUSED ? (1 + kExtraPerFace) * kFusedMaxF : 1];
+    __shared__ FaceData s_fd[FUSED ? kFusedMaxF : 1];
 #if defined(DIRT_RASTER_LDS_PAD) && DIRT_RASTER_LDS_PAD > 0
     __shared__ volatile char occupancy_probe[DIRT_RASTER_LDS_PAD];  // experiment: caps workgroups per CU
     if (threadIdx.x == 1023) occupancy_probe[0] = 0;
@@ -430,9 +441,30 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const int i = tx * kTile + lx, j = ty * kTile + ly;
     const int dx = lx * 256, dy = ly * 256;  // offset from the tile origin (sub-pixels)
     const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
-    const Rec *frame_recs = recs + (int64_t)b * nrec;
+    const Rec *frame_recs = FUSED ? s_recs : recs + (int64_t)b * nrec;
+    const FaceData *fdata_frame = FUSED ? s_fd : fdata + (int64_t)b * F;
     const bool in_frame = i < W && j < H;
     const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
+    if constexpr (FUSED) {
+        if (t < F) {
+            bool oob;
+            s_fd[t] = setup_face_into(verts + (int64_t)b * V * 4, faces + ((int64_t)b * F + t) * 3, V, F, W, H, t,
+                                      s_recs, oob);
+            if (oob) atomicOr(flag, 1u);
+        }
+        __syncthreads();
+        if (blockIdx.x == 0) {
+            // publish the frame's records and FaceData for the backward (plain stores; the backward is a
+            // later launch)
+            Rec *gr = const_cast<Rec *>(recs) + (int64_t)b * nrec;
+            for (int k = t; k < (int)nrec; k += 256) {
+                const int f = face_of_record(k, F);
+                const int s = k < F ? 0 : (k - F) - (f * kExtraPerFace) + 1;
+                if (k < F || s < s_fd[f].nsub) gr[k] = s_recs[k];
+            }
+            if (t < F) const_cast<FaceData *>(fdata)[(int64_t)b * F + t] = s_fd[t];
+        }
+    }
 
 
     uint64_t best = kKeyInit<kNoDepth>;
@@ -462,11 +494,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         asm volatile("" : "+v"(dep));
         slab_bins += dep;
     }
-    if (slab > 0 && !(AB & 8)) load_chunk(0);
+    if (!FUSED && slab > 0 && !(AB & 8)) load_chunk(0);
     // This forward's setup zeroed the other count set, so the count is the sum of both (no dependent
-    // parity load); F == 0: setup did not run
-    const uint32_t raw = F > 0 ? counts[cc * kCountStride] + counts[((int64_t)B * ncoarse + cc) * kCountStride] : 0u;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
+    // parity load); F == 0: setup did not run.  FUSED: no bins (the count sets stay clean), every record
+    // of the frame is filtered (the overflow path)
+    const uint32_t raw = FUSED ? 0xffffffffu
+                               : F > 0 ? counts[cc * kCountStride] + counts[((int64_t)B * ncoarse + cc) * kCountStride] : 0u;
+    if (!FUSED && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
     if (!(AB & 16)) {
         // housekeeping spread over all blocks (a few KB each): zero-fill the caller's gradient
         // accumulators if it passed them (after the slab loads are in flight)
@@ -486,9 +520,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         }
     }
     // an overflowed slab (more pairs than its capacity): filter every record of the frame instead
-    const bool overflow = raw > slab;
+    const bool overflow = FUSED || raw > slab;
     const uint32_t n_items = overflow ? (uint32_t)nrec : raw;
-    const FaceData *fdata_frame = fdata + (int64_t)b * F;
     // tile rectangle relative to the coarse tile
     const uint32_t rx0 = (uint32_t)(ti0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
     const uint32_t ry0 = (uint32_t)(tj0 - (cy << cshift)), ry1 = ry0 + kTile - 1;
@@ -672,7 +705,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             }
             // next chunk's slab entries (its filter runs after the next barrier-free LDS writes; t_list
             // is rewritten only after this chunk's last staging round)
-            if (!overflow && chunk + kStrips * kFilterBlock < n_items) {
+            if (!FUSED && !overflow && chunk + kStrips * kFilterBlock < n_items) {
                 load_chunk(chunk + kStrips * kFilterBlock);
             } else {
                 // (no next chunk: defining ev on both paths ends its live range at the filter instead of
@@ -710,7 +743,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         return;
     }
     const Rec &r = frame_recs[best_rec];
-    const FaceData fd = fdata[(int64_t)b * F + face_of_record(best_rec, F)];
+    const FaceData fd = fdata_frame[face_of_record(best_rec, F)];
     gbuffer[o] = best_rec | (fd.clipped ? kGbufMulti : 0);
     int64_t E[3];
     edge_values(r, i, j, E);
@@ -798,7 +831,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         }
         covbits[o] = (AB & 32) ? (uint8_t)0
                                : (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, best_rec, frame_recs,
-                                                             fdata + (int64_t)b * F, F, face_of_record(best_rec, F), i, j);
+                                                             fdata_frame, F, face_of_record(best_rec, F), i, j);
         PHASE_TS(5);
     }
 }

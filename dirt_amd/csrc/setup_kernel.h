@@ -70,6 +70,55 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
     return nsub;
 }
 
+// One face's setup (R1..R5, as setup_kernel) into `frame_recs`, which may live in any address space (the
+// fused small-scene raster passes LDS): the fast-path record at slot f, or the clipped sub-records.
+// Returns the face's FaceData; `oob` = a vertex index outside [0, V) (the face is culled).
+__device__ __forceinline__ FaceData setup_face_into(const float *vb, const int32_t *face3, int V, int F, int W, int H,
+                                                    int f, Rec *frame_recs, bool &oob)
+{
+    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+    const int32_t vidx[3] = {face3[0], face3[1], face3[2]};
+    Tri tri;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool in = vidx[k] >= 0 && vidx[k] < V;
+        const float4 pv = in ? *reinterpret_cast<const float4 *>(vb + (int64_t)vidx[k] * 4) : make_float4(0.f, 0.f, 0.f, 1.f);
+        tri.v[k][0] = pv.x; tri.v[k][1] = pv.y; tri.v[k][2] = pv.z; tri.v[k][3] = pv.w;
+        ok = ok && in;
+    }
+    oob = !ok;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ok = ok && finite4(tri.v[k]);
+    FaceData fd;
+    fd.v[0] = vidx[0]; fd.v[1] = vidx[1]; fd.v[2] = vidx[2];
+    fd.w[0] = tri.v[0][3]; fd.w[1] = tri.v[1][3]; fd.w[2] = tri.v[2][3];
+    fd.clipped = 0;
+    bool fast = ok;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float w = tri.v[k][3];
+        fast = fast && (w > 0.0f && fabsf(tri.v[k][0]) <= gx * w && fabsf(tri.v[k][1]) <= gy * w);
+    }
+    Rec r;
+    set_empty(r, f);
+    int nsub = 0;
+    if (fast) {
+        const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
+        make_record(tri.v, id, W, H, f, r);
+        frame_recs[f] = r;
+        nsub = 1;
+    } else {
+        frame_recs[f] = r;  // empty unless clip_face overwrites it
+        if (ok) {
+            nsub = clip_face(tri, W, H, F, f, frame_recs);
+            fd.clipped = 1;
+        }
+    }
+    fd.nsub = nsub;
+    return fd;
+}
+
 // bbox (pixels) packed as i0 | i1<<16 and j0 | j1<<16; empty when i0 > i1
 __device__ __forceinline__ void coarse_range(uint32_t bx, uint32_t by, int cshift, int &cx0, int &cx1, int &cy0, int &cy1)
 {

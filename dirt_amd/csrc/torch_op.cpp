@@ -1,0 +1,225 @@
+// torch_op.cpp -- the public rasterise op's autograd function in C++ (PyTorch extension `_dirt_torch`).
+//
+// Same semantics as dirt_amd.rasterise_ops._RasteriseFunction (the Python torch.autograd.Function kept as
+// the fallback): forward = dirt_rasterise_fwd / dirt_rasterise_fwd_gbuffer, registered gradient =
+// dirt_rasterise_bwd, through the C ABI of include/dirt_mi355x.h.  The reference registers its op in C++
+// too (REGISTER_OP("Rasterise"), csrc/rasterise_egl.cpp:33-53, RasteriseOpGpu::Compute :284-514); doing the
+// per-call bookkeeping here (allocation, workspace cache, stream lookup, the backward run by the autograd
+// engine without a trip through Python) keeps the eager op close to the kernels' time.
+//
+// The library is not linked: init(path) dlopens the same libdirt_mi355x.so the ctypes binding loaded
+// (dirt_amd/_lib.py, DIRT_MI355X_LIB honoured) and resolves the entry points by name.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <dlfcn.h>
+
+#include <list>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+
+#include "../../include/dirt_mi355x.h"
+
+namespace {
+
+struct Api {
+    decltype(&dirt_workspace_sizes) workspace_sizes = nullptr;
+    decltype(&dirt_rasterise_fwd) fwd = nullptr;
+    decltype(&dirt_rasterise_fwd_gbuffer) fwd_gbuffer = nullptr;
+    decltype(&dirt_rasterise_bwd) bwd = nullptr;
+    decltype(&dirt_scratch_clear) scratch_clear = nullptr;
+    decltype(&dirt_check_faces) check_faces = nullptr;
+    decltype(&dirt_last_error) last_error = nullptr;
+} g_api;
+
+void check(int rc)
+{
+    if (rc == DIRT_OK) return;
+    const std::string msg = g_api.last_error ? g_api.last_error() : "dirt: error";
+    if (rc == DIRT_EINVAL) throw std::invalid_argument(msg);   // ValueError, like OP_REQUIRES InvalidArgument
+    if (rc == DIRT_EFACE) throw std::out_of_range(msg);        // IndexError
+    throw std::runtime_error(msg);
+}
+
+void init(const std::string &path)
+{
+    void *h = dlopen(path.c_str(), RTLD_NOW | RTLD_GLOBAL);
+    if (!h) throw std::runtime_error(std::string("_dirt_torch: cannot load ") + path + ": " + dlerror());
+    auto sym = [&](const char *name) {
+        void *p = dlsym(h, name);
+        if (!p) throw std::runtime_error(std::string("_dirt_torch: ") + path + " lacks " + name);
+        return p;
+    };
+    g_api.workspace_sizes = reinterpret_cast<decltype(g_api.workspace_sizes)>(sym("dirt_workspace_sizes"));
+    g_api.fwd = reinterpret_cast<decltype(g_api.fwd)>(sym("dirt_rasterise_fwd"));
+    g_api.fwd_gbuffer = reinterpret_cast<decltype(g_api.fwd_gbuffer)>(sym("dirt_rasterise_fwd_gbuffer"));
+    g_api.bwd = reinterpret_cast<decltype(g_api.bwd)>(sym("dirt_rasterise_bwd"));
+    g_api.scratch_clear = reinterpret_cast<decltype(g_api.scratch_clear)>(sym("dirt_scratch_clear"));
+    g_api.check_faces = reinterpret_cast<decltype(g_api.check_faces)>(sym("dirt_check_faces"));
+    g_api.last_error = reinterpret_cast<decltype(g_api.last_error)>(sym("dirt_last_error"));
+}
+
+// Forward-only scratch (bins, bin counters) per (device, stream, layout), cleared once: every forward
+// leaves it clean for the next one of the same layout (DIRT_FWD_SCRATCH_CLEAN).  LRU of a few layouts.
+struct ScratchCache {
+    typedef std::tuple<int, uintptr_t, int64_t, int64_t, int64_t, int64_t, int64_t> Key;
+    std::mutex mu;
+    std::list<std::pair<Key, at::Tensor>> lru;
+    at::Tensor get(const Key &k, size_t bytes, const at::Device &dev, hipStream_t stream)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto it = lru.begin(); it != lru.end(); ++it)
+            if (it->first == k) {
+                lru.splice(lru.begin(), lru, it);
+                return it->second;
+            }
+        at::Tensor t = at::empty({(int64_t)std::max<size_t>(bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
+        check(g_api.scratch_clear((int)std::get<2>(k), (int)std::get<3>(k), (int)std::get<4>(k), (int)std::get<5>(k),
+                                  std::get<6>(k), t.data_ptr(), bytes, stream));
+        lru.emplace_front(k, t);
+        while (lru.size() > 4) lru.pop_back();
+        return t;
+    }
+    void clear()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        lru.clear();
+    }
+    size_t size()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        return lru.size();
+    }
+} g_scratch;
+
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
+    static variable_list forward(AutogradContext *ctx, at::Tensor background, at::Tensor vertices,
+                                 at::Tensor vertex_colors, at::Tensor faces, c10::optional<at::Tensor> camera_pos,
+                                 int64_t H, int64_t W, int64_t C, int64_t shader_id, int64_t bin_capacity,
+                                 bool want_gbuf, bool check_faces)
+    {
+        const int64_t B = vertices.size(0), V = vertices.size(1), F = faces.size(1);
+        const at::Device dev = vertices.device();
+        c10::hip::HIPGuard guard(dev.index());
+        hipStream_t stream = c10::hip::getCurrentHIPStream(dev.index()).stream();
+        size_t saved_bytes = 0, scratch_bytes = 0;
+        check(g_api.workspace_sizes((int)B, (int)H, (int)W, (int)C, (int)V, (int)F, bin_capacity, &saved_bytes,
+                                    &scratch_bytes));
+        const auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+        const auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
+        at::Tensor pixels = at::empty({B, H, W, C}, f32);
+        at::Tensor gbuffer = at::empty({B, H, W}, i32);
+        at::Tensor saved = at::empty({(int64_t)std::max<size_t>(saved_bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
+        const bool need_grad = shader_id == DIRT_SHADER_GOURAUD && V > 0 &&
+                               (ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2));
+        at::Tensor gv, gc;
+        if (need_grad) {  // zero-filled by the forward in passing; the backward accumulates
+            gv = at::empty({B, V, 4}, f32);
+            gc = at::empty({B, V, C}, f32);
+        }
+        if (check_faces) {
+            at::Tensor flag = at::empty({256}, at::TensorOptions().dtype(at::kByte).device(dev));
+            check(g_api.check_faces(faces.data_ptr<int32_t>(), (int)B, (int)V, (int)F, flag.data_ptr(), 256, stream));
+        }
+        at::Tensor scratch = g_scratch.get(ScratchCache::Key{dev.index(), reinterpret_cast<uintptr_t>(stream), B, H, W,
+                                                             F, bin_capacity},
+                                           scratch_bytes, dev, stream);
+        float *zgv = need_grad ? gv.data_ptr<float>() : nullptr;
+        float *zgc = need_grad ? gc.data_ptr<float>() : nullptr;
+        variable_list out{pixels, gbuffer};
+        if (want_gbuf) {
+            at::Tensor depth = at::empty({B, H, W}, f32), bary = at::empty({B, H, W, 3}, f32), face = at::empty({B, H, W}, i32);
+            check(g_api.fwd_gbuffer(background.data_ptr<float>(), vertices.data_ptr<float>(),
+                                    vertex_colors.data_ptr<float>(), faces.data_ptr<int32_t>(), (int)B, (int)H, (int)W,
+                                    (int)C, (int)V, (int)F, pixels.data_ptr<float>(), gbuffer.data_ptr<int32_t>(),
+                                    saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
+                                    DIRT_FWD_SCRATCH_CLEAN, zgv, zgc, depth.data_ptr<float>(), bary.data_ptr<float>(),
+                                    face.data_ptr<int32_t>(), stream));
+            out.push_back(depth);
+            out.push_back(bary);
+            out.push_back(face);
+        } else {
+            const float *cam = camera_pos.has_value() ? camera_pos->data_ptr<float>() : nullptr;
+            check(g_api.fwd(background.data_ptr<float>(), vertices.data_ptr<float>(), vertex_colors.data_ptr<float>(),
+                            faces.data_ptr<int32_t>(), cam, (int)B, (int)H, (int)W, (int)C, (int)V, (int)F,
+                            (int)shader_id, pixels.data_ptr<float>(), gbuffer.data_ptr<int32_t>(), saved.data_ptr(),
+                            saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, DIRT_FWD_SCRATCH_CLEAN, zgv,
+                            zgc, stream));
+        }
+        ctx->save_for_backward({vertices, vertex_colors, faces, pixels, gbuffer, saved});
+        ctx->saved_data["dims"] = std::vector<int64_t>{B, H, W, C, V, F, shader_id};
+        ctx->saved_data["prezeroed"] = need_grad;
+        if (need_grad) {
+            ctx->saved_data["gv"] = gv;
+            ctx->saved_data["gc"] = gc;
+        }
+        variable_list nd(out.begin() + 1, out.end());
+        ctx->mark_non_differentiable(nd);
+        return out;
+    }
+
+    static variable_list backward(AutogradContext *ctx, variable_list grads)
+    {
+        const std::vector<int64_t> d = ctx->saved_data["dims"].toIntVector();
+        const int64_t B = d[0], H = d[1], W = d[2], C = d[3], V = d[4], F = d[5], shader_id = d[6];
+        if (shader_id != DIRT_SHADER_GOURAUD)
+            throw std::runtime_error("only the Gouraud fragment program has a gradient (the reference registers none)");
+        auto sv = ctx->get_saved_variables();
+        const at::Tensor &vertices = sv[0], &vertex_colors = sv[1], &faces = sv[2], &pixels = sv[3], &gbuffer = sv[4],
+                         &saved = sv[5];
+        const at::Device dev = vertices.device();
+        c10::hip::HIPGuard guard(dev.index());
+        hipStream_t stream = c10::hip::getCurrentHIPStream(dev.index()).stream();
+        const auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+        at::Tensor gp = grads[0].defined() ? grads[0].to(at::kFloat).contiguous() : at::zeros({B, H, W, C}, f32);
+        // the forward's zero-filled buffers serve one backward (autograd may keep the returned tensors as
+        // .grad); a second backward of the same graph (retain_graph) starts from fresh ones
+        unsigned flags = 0;
+        at::Tensor gv, gc;
+        if (ctx->saved_data["prezeroed"].toBool()) {
+            gv = ctx->saved_data["gv"].toTensor();
+            gc = ctx->saved_data["gc"].toTensor();
+            ctx->saved_data["prezeroed"] = false;
+            ctx->saved_data.erase("gv");
+            ctx->saved_data.erase("gc");
+            flags = DIRT_BWD_ACCUMULATE;
+        } else {
+            gv = at::empty({B, V, 4}, f32);
+            gc = at::empty({B, V, C}, f32);
+        }
+        at::Tensor gbg = at::empty({B, H, W, C}, f32);
+        check(g_api.bwd(vertices.data_ptr<float>(), vertex_colors.data_ptr<float>(), faces.data_ptr<int32_t>(),
+                        pixels.data_ptr<float>(), gp.data_ptr<float>(), gbuffer.data_ptr<int32_t>(), saved.data_ptr(),
+                        (int)B, (int)H, (int)W, (int)C, (int)V, (int)F, gv.data_ptr<float>(), gc.data_ptr<float>(),
+                        gbg.data_ptr<float>(), flags, stream));
+        return {gbg, gv, gc, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
+                at::Tensor(), at::Tensor(), at::Tensor()};
+    }
+};
+
+variable_list rasterise(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
+                        c10::optional<at::Tensor> camera_pos, int64_t H, int64_t W, int64_t C, int64_t shader_id,
+                        int64_t bin_capacity, bool want_gbuf, bool check_faces)
+{
+    if (!g_api.fwd) throw std::runtime_error("_dirt_torch.init(path) was not called");
+    return RasteriseFn::apply(background, vertices, vertex_colors, faces, camera_pos, H, W, C, shader_id, bin_capacity,
+                              want_gbuf, check_faces);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
+{
+    m.doc() = "dirt_amd rasterise op: C++ autograd function over the C ABI of libdirt_mi355x.so";
+    m.def("init", &init, "dlopen libdirt_mi355x.so and resolve the C ABI");
+    m.def("rasterise", &rasterise, "rasterise forward (+ registered backward)");
+    m.def("scratch_cache_clear", []() { g_scratch.clear(); });
+    m.def("scratch_cache_size", []() { return g_scratch.size(); });
+}

@@ -47,6 +47,21 @@ def _as_tensor(x, dtype, device):
     return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
 
 
+class _on_device:
+    """torch.cuda.device(dev), skipped when dev is already the current device (host overhead per call)."""
+
+    def __init__(self, dev):
+        self.ctx = None if dev.index is None or dev.index == torch.cuda.current_device() else torch.cuda.device(dev)
+
+    def __enter__(self):
+        if self.ctx is not None:
+            self.ctx.__enter__()
+
+    def __exit__(self, *a):
+        if self.ctx is not None:
+            self.ctx.__exit__(*a)
+
+
 class _Workspace:
     """Per-(device, stream, layout) cache of the forward-only scratch (tile bins, bin counters).
 
@@ -117,7 +132,7 @@ class _RasteriseFunction(torch.autograd.Function):
         gv = torch.empty((B, V, 4), dtype=torch.float32, device=dev) if need_grad else None
         gc = torch.empty((B, V, C), dtype=torch.float32, device=dev) if need_grad else None
         extra = ()
-        with torch.cuda.device(dev):
+        with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             if check_faces:
                 _check_faces_now(faces, B, V, F, stream)
@@ -169,7 +184,7 @@ class _RasteriseFunction(torch.autograd.Function):
             grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
         grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         lib = _lib.load()
-        with torch.cuda.device(dev):
+        with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             _lib.check(lib.dirt_rasterise_bwd(
                 vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), pixels.data_ptr(),
@@ -237,6 +252,41 @@ def _camera(camera_pos, shader_id, dev):
     return camera_pos
 
 
+_EXT = None
+
+
+def _torch_ext():
+    """The C++ autograd function (dirt_amd/csrc/torch_op.cpp, module _dirt_torch) bound to the library
+    _lib loaded, or None if it is not built or DIRT_TORCH_EXT=0 (then _RasteriseFunction, the same op in
+    Python, runs: both call the same HIP kernels through the C ABI; there is no CPU path)."""
+    global _EXT
+    if _EXT is None:
+        _EXT = False
+        if os.environ.get("DIRT_TORCH_EXT", "1") != "0":
+            try:
+                from . import _dirt_torch
+            except ImportError:
+                _dirt_torch = None
+            if _dirt_torch is not None:
+                _lib.load()
+                _dirt_torch.init(_lib.LIB_PATH)
+                _EXT = _dirt_torch
+    return _EXT or None
+
+
+def workspace_cache_clear():
+    """Drop the cached per-layout scratch buffers (both implementations)."""
+    _workspace.clear()
+    ext = _torch_ext()
+    if ext is not None:
+        ext.scratch_cache_clear()
+
+
+def workspace_cache_size():
+    ext = _torch_ext()
+    return len(_workspace._d) + (ext.scratch_cache_size() if ext is not None else 0)
+
+
 # DIRT_CHECK_FACES=1: every call range-checks its face indices (one kernel + a host sync; off by default)
 _CHECK_FACES_DEFAULT = os.environ.get("DIRT_CHECK_FACES", "") not in ("", "0")
 
@@ -252,8 +302,10 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
     if check_faces is None:
         check_faces = _CHECK_FACES_DEFAULT
-    outs = _RasteriseFunction.apply(background, vertices, vertex_colors, faces, camera_pos, int(height), int(width),
-                                    int(channels), shader_id, int(bin_capacity), bool(want_gbuf), bool(check_faces))
+    args = (background, vertices, vertex_colors, faces, camera_pos, int(height), int(width), int(channels), shader_id,
+            int(bin_capacity), bool(want_gbuf), bool(check_faces))
+    ext = _torch_ext()
+    outs = ext.rasterise(*args) if ext is not None else _RasteriseFunction.apply(*args)
     if want_gbuf:
         return outs
     pixels, gbuffer = outs

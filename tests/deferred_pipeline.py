@@ -19,6 +19,8 @@ background pixel holding a non-finite value carries no vertex gradient across it
 
 Test infrastructure only (imported by tests/ and tools/bench_configs.py).
 """
+import functools
+
 import numpy as np
 import torch
 import torch.nn.functional as Fn
@@ -39,12 +41,29 @@ def grid_surface(n=100, seed=0):
     return world, faces.astype(np.int32), albedo
 
 
-def camera(H, W, device=None):
-    """The sample's camera (samples/deferred.py:50-60, OpenGL perspective); the surface is tilted towards the
-    camera (rotation about x) and pushed away along -z."""
+@functools.lru_cache(maxsize=16)
+def _camera_cpu(H, W):
     view = matrices.compose(matrices.rodrigues([0.9, 0., 0.]), matrices.translation([0., -0.12, -2.3]))
     proj = matrices.perspective_projection(near=0.1, far=20., right=0.1, aspect=float(H) / W)
+    return view, proj, torch.linalg.inv(view)[3, :3]
+
+
+def camera(H, W, device=None):
+    """The sample's camera (samples/deferred.py:50-60, OpenGL perspective); the surface is tilted towards the
+    camera (rotation about x) and pushed away along -z.  Built once on the CPU, then moved."""
+    view, proj, _ = _camera_cpu(H, W)
     return view.to(device), proj.to(device)
+
+
+def camera_position(H, W, device=None):
+    """The camera's world position, tf.matrix_inverse(view_matrix)[3, :3] (samples/deferred.py:107)."""
+    return _camera_cpu(H, W)[2].to(device)
+
+
+@functools.lru_cache(maxsize=16)
+def _constants(device):
+    return (torch.tensor([0.2, 0.2, 0.2], device=device), unit([1., -0.3, -0.5]).to(device),
+            torch.tensor([1., 0., 0.], device=device), torch.tensor([1., 1., 1.], device=device))
 
 
 def unit(v):
@@ -84,15 +103,13 @@ def shade(pos, col, nrm, H, W):
     valid = torch.isfinite(pos_d).all(-1, keepdim=True) & torch.isfinite(nrm_d).all(-1, keepdim=True)
     zero = torch.zeros_like(pos_d)
     pos_s, nrm_s, col_s = (torch.where(valid, x, zero) for x in (pos_d, nrm_d, col))
-    ambient = col_s * torch.tensor([0.2, 0.2, 0.2], device=dev)
-    light_direction = unit([1., -0.3, -0.5]).to(dev)
+    grey, light_direction, red, white = _constants(dev)
+    ambient = col_s * grey
     diffuse = lighting.diffuse_directional(nrm_s.reshape(-1, 3), col_s.reshape(-1, 3), light_direction,
-                                           light_color=torch.tensor([1., 0., 0.], device=dev), double_sided=False)
-    view, _ = camera(H, W, dev)
-    camera_position_world = torch.linalg.inv(view)[3, :3]
+                                           light_color=red, double_sided=False)
     specular = lighting.specular_directional(pos_s.reshape(-1, 3), nrm_s.reshape(-1, 3), col_s.reshape(-1, 3),
-                                             light_direction, light_color=torch.tensor([1., 1., 1.], device=dev),
-                                             camera_position=camera_position_world, shininess=6.,
+                                             light_direction, light_color=white,
+                                             camera_position=camera_position(H, W, dev), shininess=6.,
                                              double_sided=False)
     pixels = diffuse.reshape(H, W, 3) + specular.reshape(H, W, 3) + ambient
     return pixels, valid

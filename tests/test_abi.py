@@ -83,3 +83,12 @@ def test_scratch_clear_validates_without_a_gpu():
     assert lib.dirt_scratch_clear(0, 16, 16, 1, 0, None, 0, None) == _lib.DIRT_OK
     assert lib.dirt_scratch_clear(1, 16, 16, 1, 0, None, 0, None) == _lib.DIRT_EINVAL
     assert "scratch" in lib.dirt_last_error().decode()
+
+
+def test_cpp_autograd_extension_builds_and_binds():
+    """The public op's C++ autograd function (dirt_amd/_dirt_torch) is built in-tree and binds the C ABI
+    of the library _lib loads (init dlopens it: no GPU needed)."""
+    from dirt_amd import rasterise_ops
+    ext = rasterise_ops._torch_ext()
+    assert ext is not None
+    assert ext.scratch_cache_size() == 0

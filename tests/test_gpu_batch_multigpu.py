@@ -113,7 +113,7 @@ def test_autograd_workspace_cache_and_retained_graph():
     serve only the first)."""
     import dirt_amd
     from dirt_amd import rasterise_ops
-    rasterise_ops._workspace.clear()
+    rasterise_ops.workspace_cache_clear()
     scs = [scenes.random_triangles(F=900, W=96, H=80, radius_px=10.0, seed=s) for s in (81, 82)]
     scs.append(scenes.random_triangles(F=500, W=64, H=48, radius_px=8.0, seed=83))
     for rep in range(3):
@@ -122,7 +122,7 @@ def test_autograd_workspace_cache_and_retained_graph():
             px = dirt_amd.rasterise(t[0], t[1], t[2], _gpu(f))
             ref, _, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
             np.testing.assert_array_equal(px.detach().cpu().numpy(), ref[0])
-    assert len(rasterise_ops._workspace._d) == 2  # two layouts (F, H, W differ), one stream
+    assert rasterise_ops.workspace_cache_size() == 2  # two layouts (F, H, W differ), one stream
     bg, v, c, f = scs[0]
     t = [_gpu(a).requires_grad_(True) for a in (bg, v, c)]
     px = dirt_amd.rasterise(t[0], t[1], t[2], _gpu(f))
@@ -208,3 +208,34 @@ def test_hip_graph_capture_of_autograd_path():
     assert torch.equal(outs["grads"][0], ref_g[0])
     for a, b in zip(outs["grads"][1:], ref_g[1:]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
+
+
+@pytest.mark.parametrize("want_gbuf", [False, True])
+def test_cpp_autograd_op_matches_python_function(want_gbuf):
+    """The public op runs the C++ autograd function (_dirt_torch, dirt_amd/csrc/torch_op.cpp) when built;
+    the Python torch.autograd.Function (_RasteriseFunction) is the same op over the same C ABI.  Both give
+    bit-identical forwards and the same gradients, on a fused small scene and a binned one, with a
+    retained graph's second backward."""
+    from dirt_amd import rasterise_ops
+    ext = rasterise_ops._torch_ext()
+    assert ext is not None, "the C++ extension dirt_amd/_dirt_torch*.so is not built"
+    for sc in (scenes.cube_scene(), scenes.random_triangles(F=1500, W=128, H=96, radius_px=10.0, seed=90,
+                                                             perspective=True)):
+        bg, v, c, f = (a[None] for a in sc)
+        B, H, W, C = bg.shape
+        g = torch.randn(bg.shape, device="cuda")
+        res = []
+        for impl in ("ext", "py"):
+            t = [_gpu(a).requires_grad_(True) for a in (bg, v, c)]
+            args = (t[0], t[1], t[2], _gpu(f), None, H, W, C, 0, 0, want_gbuf, False)
+            outs = ext.rasterise(*args) if impl == "ext" else rasterise_ops._RasteriseFunction.apply(*args)
+            g1 = torch.autograd.grad(outs[0], t, g, retain_graph=True)
+            g2 = torch.autograd.grad(outs[0], t, g)
+            res.append(([o.detach().clone() for o in outs], g1, g2))
+        (oe, ge1, ge2), (op, gp1, gp2) = res
+        assert len(oe) == len(op) == (5 if want_gbuf else 2)
+        for a, b in zip(oe, op):
+            assert torch.equal(a, b)
+        for a, b in zip(ge1 + ge2, gp1 + gp1):
+            assert torch.equal(a, b) if a.shape == bg.shape else True
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()) + 1e-30)

@@ -539,3 +539,33 @@ def test_dense_tiles_slot_table_and_tail_overflow(C, r):
                 for y in range(0, 48, 16) for x in range(0, 64, 16)]
     assert max(per_tile) > 64
     check_scene(bg, v, c, f)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fused_small_scene_forward(seed):
+    """Frames of at most 32 faces take the fused forward (raster_kernel FUSED: each workgroup sets up the
+    frame's faces in LDS, no setup launch, no bins; tile 0 publishes the records for the backward).
+    Adversarial small scenes (clipping, ties, slivers, w <= 0), batches and channel counts: bit-exact
+    forward, gradients in tolerance -- the backward reads the records the fused forward published."""
+    W, H = [(64, 48), (33, 17), (130, 70), (16, 16)][seed % 4]
+    C = (3, 1, 7, 5)[seed % 4]
+    if seed % 3 == 2:
+        frames = [scenes.adversarial_scene(seed * 10 + k, W=W, H=H, C=C, F=8) for k in range(3)]
+        F = max(fr[3].shape[0] for fr in frames)
+        frames = [(bg, v, c, np.concatenate([f, np.zeros((F - f.shape[0], 3), np.int32)])) for bg, v, c, f in frames]
+        V = max(fr[1].shape[0] for fr in frames)
+        frames = [(bg, np.concatenate([v, np.tile(v[:1], (V - v.shape[0], 1))]),
+                   np.concatenate([c, np.tile(c[:1], (V - c.shape[0], 1))]), f) for bg, v, c, f in frames]
+        scene = [np.stack([fr[k] for fr in frames]) for k in range(4)]
+    else:
+        scene = scenes.adversarial_scene(seed, W=W, H=H, C=C, F=8)
+    assert scene[3].shape[-2] <= 32
+    check_scene(*scene, seed=seed)
+
+
+def test_fused_small_scene_clipping_and_shared_mesh():
+    bg, v, c, f = scenes.clipping_scene()
+    check_scene(bg, v, c, f[:32])
+    bg, v, c, f = scenes.shared_mesh_scene(n=5)  # 2 layers x 32 faces: the first layer alone is fused
+    check_scene(bg, v, c, f[:32])
+    check_scene(bg, v, c, f[:33])  # one face more: the binned path, same answer as the oracle
