@@ -50,11 +50,16 @@ def gather_frames_async(local, batch, group=None):
     else:
         pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         pad[: local.shape[0]] = local
-    out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    work = dist.all_gather_into_tensor(out, pad, group=group, async_op=True)
+    via_host = pad.is_cuda and dist.get_backend(group) == "gloo"  # gloo moves host memory only
+    src = pad.cpu() if via_host else pad
+    out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=src.device)
+    work = dist.all_gather_into_tensor(out, src, group=group, async_op=True)
 
     def finish():
+        nonlocal out
         work.wait()
+        if via_host:
+            out = out.to(local.device)
         if all(hi - lo == mx for lo, hi in sizes):
             return out
         return torch.cat([out[r * mx: r * mx + hi - lo] for r, (lo, hi) in enumerate(sizes)], 0)

@@ -12,6 +12,6 @@ timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-budget 8 > $out/
 rc=$?; echo "bench rc=$rc"; cat $out/bench_$tag.json; tail -5 $out/bench_$tag.err
 [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/prof_$tag -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-graph > $GRAFT_REPO_ROOT/$out/prof_$tag.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/prof_$tag -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-graph --rotate 0 --no-api-leg > $GRAFT_REPO_ROOT/$out/prof_$tag.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -5 $GRAFT_REPO_ROOT/$out/prof_$tag.log
 exit $rc

@@ -63,8 +63,18 @@ def main():
     for k, name in enumerate(names):
         print("  %-32s median %7.0f  p90 %7.0f ticks  (%4.1f%% of the median lifetime)" % (
             name, np.median(d[:, k]), np.percentile(d[:, k], 90), 100.0 * np.median(d[:, k]) / np.median(life)))
-    print("  lifetime median %.0f ticks, p90 %.0f; starts spread %.0f ticks (rebased per XCC)" % (
-        np.median(life), np.percentile(life, 90), np.percentile(T[:, 0] - T[:, 0].min(), 90)))
+    xcc = ts[:, 9].astype(np.int64) & 0xf
+    st, en = [], []
+    for x in np.unique(xcc):
+        m = xcc == x
+        t0 = T[m, 0].min()
+        st.append(T[m, 0] - t0)
+        en.append(T[m, 4] - t0)
+    st, en = np.concatenate(st), np.concatenate(en)
+    print("  lifetime median %.0f ticks, p90 %.0f; per XCC: starts p50 / p90 / max %.0f / %.0f / %.0f, ends p50 / "
+          "max %.0f / %.0f ticks after the XCC's first start" % (
+              np.median(life), np.percentile(life, 90), np.median(st), np.percentile(st, 90), st.max(),
+              np.median(en), en.max()))
 
 
 if __name__ == "__main__":
