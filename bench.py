@@ -280,8 +280,17 @@ def main():
         roofline["traffic_frac"] = round(traffic / (kern_us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
 
     legs = {}
-    # ---- leg: the public op surface (dirt_amd.rasterise_batch + torch.autograd), eager and graph-captured
-    if not args.no_api_leg:
+
+    def leg(name, fn):
+        """Run one extra leg; a failure is reported in the JSON line instead of ending the run (the headline
+        `value` above is already measured)."""
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 -- any leg failure is data, not a reason to lose the line
+            legs[name] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
+            torch.cuda.synchronize()
+
+    def api_leg():
         import dirt_amd
         bg_r, v_r, c_r = (t.clone().requires_grad_(True) for t in (bg, v, c))
 
@@ -301,11 +310,16 @@ def main():
             "eager_mpix_s": round(world * B * H * W * n_api / t_eager / 1e6, 1),
             "eager_ms_per_step": round(t_eager * 1e3 / n_api, 4),
             "graph_mpix_s": round(world * B * H * W * n_api / t_graph / 1e6, 1),
-            "graph_ms_per_step": round(t_graph * 1e3 / n_api, 4)}
+            "graph_ms_per_step": round(t_graph * 1e3 / n_api, 4),
+            "impl": "C++ autograd function (_dirt_torch)" if dirt_amd.rasterise_ops._torch_ext() is not None
+                    else "Python torch.autograd.Function"}
         del g_api
 
-    # ---- leg: rotating distinct frames, working set past the 256 MiB Infinity Cache (cold HBM)
-    if args.rotate > 1:
+    # ---- leg: the public op surface (dirt_amd.rasterise_batch + torch.autograd), eager and graph-captured
+    if not args.no_api_leg:
+        leg("api_autograd", api_leg)
+
+    def cold_leg():
         R = args.rotate
         rot = []
         for k in range(R):
@@ -339,8 +353,11 @@ def main():
             "grad_kernel_frac": round(kbytes["grad_kernel"] / (kr["grad_kernel"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
         del g_rot, rot
 
-    # ---- leg (N > 1): the output all-gather over RCCL / xGMI, alone and overlapped with the next step
-    if world > 1 and not args.no_gather_leg:
+    # ---- leg: rotating distinct frames, working set past the 256 MiB Infinity Cache (cold HBM)
+    if args.rotate > 1:
+        leg("cold_cache", cold_leg)
+
+    def gather_leg():
         from dirt_amd.sharding import gather_frames_async
         batch = world * B
         for _ in range(3):
@@ -389,6 +406,10 @@ def main():
             "recv_GBps_per_rank": round(recv / (t_g / n_g) / 1e9, 1),
             "value_with_gather": round(world * B * H * W * args.steps / t_p / 1e6, 1),
             "ms_per_step_with_gather": round(t_p * 1e3 / args.steps, 4)}
+
+    # ---- leg (N > 1): the output all-gather over RCCL / xGMI, alone and overlapped with the next step
+    if world > 1 and not args.no_gather_leg:
+        leg("gather", gather_leg)
 
     cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -103,7 +103,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
     static variable_list forward(AutogradContext *ctx, at::Tensor background, at::Tensor vertices,
                                  at::Tensor vertex_colors, at::Tensor faces, c10::optional<at::Tensor> camera_pos,
                                  int64_t H, int64_t W, int64_t C, int64_t shader_id, int64_t bin_capacity,
-                                 bool want_gbuf, bool check_faces)
+                                 bool want_gbuf, bool check_faces, bool grad_possible)
     {
         const int64_t B = vertices.size(0), V = vertices.size(1), F = faces.size(1);
         const at::Device dev = vertices.device();
@@ -117,7 +117,9 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
         at::Tensor pixels = at::empty({B, H, W, C}, f32);
         at::Tensor gbuffer = at::empty({B, H, W}, i32);
         at::Tensor saved = at::empty({(int64_t)std::max<size_t>(saved_bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
-        const bool need_grad = shader_id == DIRT_SHADER_GOURAUD && V > 0 &&
+        // (needs_input_grad is only defined when the node records a graph: grad_possible, decided outside
+        // forward where GradMode is visible)
+        const bool need_grad = grad_possible && shader_id == DIRT_SHADER_GOURAUD && V > 0 &&
                                (ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2));
         at::Tensor gv, gc;
         if (need_grad) {  // zero-filled by the forward in passing; the backward accumulates
@@ -200,7 +202,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
                         (int)B, (int)H, (int)W, (int)C, (int)V, (int)F, gv.data_ptr<float>(), gc.data_ptr<float>(),
                         gbg.data_ptr<float>(), flags, stream));
         return {gbg, gv, gc, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
-                at::Tensor(), at::Tensor(), at::Tensor()};
+                at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
     }
 };
 
@@ -209,8 +211,10 @@ variable_list rasterise(at::Tensor background, at::Tensor vertices, at::Tensor v
                         int64_t bin_capacity, bool want_gbuf, bool check_faces)
 {
     if (!g_api.fwd) throw std::runtime_error("_dirt_torch.init(path) was not called");
+    const bool grad_possible = at::GradMode::is_enabled() &&
+                               (background.requires_grad() || vertices.requires_grad() || vertex_colors.requires_grad());
     return RasteriseFn::apply(background, vertices, vertex_colors, faces, camera_pos, H, W, C, shader_id, bin_capacity,
-                              want_gbuf, check_faces);
+                              want_gbuf, check_faces, grad_possible);
 }
 
 }  // namespace

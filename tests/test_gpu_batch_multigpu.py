@@ -239,3 +239,22 @@ def test_cpp_autograd_op_matches_python_function(want_gbuf):
         for a, b in zip(ge1 + ge2, gp1 + gp1):
             assert torch.equal(a, b) if a.shape == bg.shape else True
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()) + 1e-30)
+
+
+def test_public_op_without_gradients():
+    """Inputs that need no gradient, and calls under torch.no_grad(): no graph is recorded, no gradient
+    buffers are zero-filled, the forward is the same."""
+    import dirt_amd
+    bg, v, c, f = scenes.random_triangles(F=800, W=80, H=64, radius_px=9.0, seed=91)
+    ref, _, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
+    px = dirt_amd.rasterise(_gpu(bg), _gpu(v), _gpu(c), _gpu(f))
+    assert not px.requires_grad
+    np.testing.assert_array_equal(px.cpu().numpy(), ref[0])
+    t = [_gpu(a).requires_grad_(True) for a in (bg, v, c)]
+    with torch.no_grad():
+        px = dirt_amd.rasterise(t[0], t[1], t[2], _gpu(f))
+    assert not px.requires_grad
+    np.testing.assert_array_equal(px.cpu().numpy(), ref[0])
+    px = dirt_amd.rasterise(t[0].detach(), t[1], t[2].detach(), _gpu(f))  # only vertices need a gradient
+    (gv,) = torch.autograd.grad(px, [t[1]], torch.ones_like(px))
+    assert torch.isfinite(gv).all()

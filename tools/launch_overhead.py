@@ -59,3 +59,31 @@ for mode in ("graph", "eager", "graph1"):
     b_, a_ = np.polyfit(ks, w, 1)
     print("%-7s " % mode + "  ".join("K=%d %.0f us" % (k, x) for k, x in zip(ks, w)) +
           "   fit: %.1f us + %.2f us/step" % (a_, b_))
+
+# the same K-step graph launched three ways: torch's replay(); after hipGraphUpload (the executable graph's
+# device-side resources set up ahead of the timed window); hipGraphLaunch through ctypes (no torch wrapper)
+import ctypes  # noqa: E402
+
+hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+hip.hipGraphLaunch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+for K in (20, 200):
+    g = bench.graph_of(step, K, s)
+    ex = ctypes.c_void_p(g.raw_cuda_graph_exec())
+    st = ctypes.c_void_p(s.cuda_stream)
+    out = []
+    for mode in ("replay", "upload+replay", "ctypes launch"):
+        walls = []
+        for rep in range(7):
+            if mode == "upload+replay":
+                assert hip.hipGraphUpload(ex, st) == 0
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if mode == "ctypes launch":
+                assert hip.hipGraphLaunch(ex, st) == 0
+            else:
+                g.replay()
+            torch.cuda.synchronize()
+            walls.append(time.perf_counter() - t0)
+        out.append("%s %.0f us" % (mode, float(np.median(walls)) * 1e6))
+    print("K=%d: " % K + ", ".join(out))
