@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
 # measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc passes of this bench at c3;
 # produced by tools/gpu_traffic.sh + tools/pmc_traffic.py, committed with the round's profiles)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "traffic.json")
 
 CONFIGS = {
     # name: (B per rank, H, W, C, F, radius_px)
@@ -132,7 +132,10 @@ def parity(sess, ref):
 
 def graph_of(fn, n, stream):
     """Capture n calls of fn into one HIP graph on `stream` (warmed on the same stream first, so cached
-    workspaces keyed by stream are hit instead of allocated inside the capture)."""
+    workspaces keyed by stream are hit instead of allocated inside the capture).  `stream` first waits for
+    the current stream: a session's buffers are stream-ordered, and steps still in flight there must not
+    overlap the warm-up call's reuse of them."""
+    stream.wait_stream(torch.cuda.current_stream(stream.device))
     with torch.cuda.stream(stream):
         fn()
     torch.cuda.synchronize()
