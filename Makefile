@@ -50,7 +50,7 @@ variant: $(HIP_DEPS)
 	mkdir -p build/variants && $(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o build/variants/$(NAME).so $(HIP_SRC)
 
 asm: $(HIP_DEPS)
-	mkdir -p build/asm && cd build/asm && $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o dirt_raster.s ../../$(HIP_SRC)
+	mkdir -p build/asm && cd build/asm && $(HIPCC) $(HIPFLAGS) $(DEFS) --cuda-device-only -S -o $(or $(NAME),dirt_raster).s ../../$(HIP_SRC)
 
 clean:
 	rm -f $(LIB) $(ORACLE) $(TORCH_EXT)

@@ -116,7 +116,8 @@ struct SlotTable {
     int32_t e[3][kSlots];      // small records: E + owned at the halo origin pixel (see kGradSmallEdge)
     uint32_t bx[kSlots], by[kSlots];  // i0 | i1 << 16 (bit 31: large record, use the global Rec)
     int32_t v[3][kSlots];    // vertex ids, indexed by list position
-    float iw[3][kSlots], w[3][kSlots];  // interpolation data of the record (own-pixel path)
+    float q[3][kSlots];      // FaceData.q of the record's face: 1/w (non-clipped face), parent clip w
+                             // (clipped face: the record's own 1/w are read from the record)
     float h2d[kSlots];                  // 1 / (2 D), D = E0 + E1 + E2 (constant over the plane)
     int32_t n;
 };
@@ -426,8 +427,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             const int32_t ri = T.key[sf] & kGbufIndexMask;
             ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
             fd = fdata_frame[face_of_record(ri, F)];
-            const Rec &r = frame_recs[ri];
-            riw0 = r.iw[0]; riw1 = r.iw[1]; riw2 = r.iw[2];
+            // 1/w of a non-clipped face: its FaceData's q (a clipped record's own 1/w, in the record's second
+            // half, are read in phase B by the lanes that show it)
+            riw0 = fd.q[0]; riw1 = fd.q[1]; riw2 = fd.q[2];
         }
         // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
         // bottom row of the halo (their one pair into the tile); nothing reads the others
@@ -454,13 +456,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             for (int k = 0; k < 3; ++k) {
                 T.A[k][sf] = ep.A[k]; T.B[k][sf] = ep.B[k];
                 T.v[k][t] = fd.v[k];  // by list position (read only by the flush)
-                T.w[k][sf] = fd.w[k];
                 small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
                         ep.B[k] < kGradSmallEdge;
                 T.e[k][sf] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
             }
-            T.iw[0][sf] = riw0; T.iw[1][sf] = riw1; T.iw[2][sf] = riw2;
-            T.h2d[sf] = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
+            T.q[0][sf] = riw0; T.q[1][sf] = riw1; T.q[2][sf] = riw2;
+            T.h2d[sf] = 0.5f / (float)ep.D;  // (E_0 + E_1 + E_2 = D at every pixel)
             T.bx[sf] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
             T.by[sf] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
         }
@@ -509,18 +510,25 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         if (sp >= 0) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { mA[k] = T.A[k][sp]; mB[k] = T.B[k][sp]; }
-            iw0 = T.iw[0][sp]; iw1 = T.iw[1][sp]; iw2 = T.iw[2][sp];
+            iw0 = T.q[0][sp]; iw1 = T.q[1][sp]; iw2 = T.q[2][sp];  // (1/w unless clipped)
             h2d = T.h2d[sp];
             me_small = !slot_is_large(T, sp);
+            if (__builtin_amdgcn_ballot_w64(multi) != 0 && multi) {
+                const Rec &rr = rec();
+                iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
+            }
         } else {
             const Rec &rr = rec();
             const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
 #pragma unroll
             for (int k = 0; k < 3; ++k) { mA[k] = me.A[k]; mB[k] = me.B[k]; }
-            iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
-            int64_t E0[3];
-            edge_values(me, i, j, E0);
-            h2d = 0.5f / (float)(E0[0] + E0[1] + E0[2]);
+            if (multi) {
+                iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
+            } else {
+                const FaceData &fq = fdata_frame[f];
+                iw0 = fq.q[0]; iw1 = fq.q[1]; iw2 = fq.q[2];
+            }
+            h2d = 0.5f / (float)me.D;
             me_small = false;
         }
         if (me_small) {
@@ -654,9 +662,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                 if (!fast_lambda(rec(), multi, m[0], m[1], m[2], lm)) continue;
                 // clip w of the parent vertices, read here (clipped faces only) to keep them out of
                 // the registers of the common path
-                const float w0 = sp >= 0 ? T.w[0][sp] : fdata_frame[f].w[0];
-                const float w1 = sp >= 0 ? T.w[1][sp] : fdata_frame[f].w[1];
-                const float w2 = sp >= 0 ? T.w[2][sp] : fdata_frame[f].w[2];
+                const float w0 = sp >= 0 ? T.q[0][sp] : fdata_frame[f].q[0];
+                const float w1 = sp >= 0 ? T.q[1][sp] : fdata_frame[f].q[1];
+                const float w2 = sp >= 0 ? T.q[2][sp] : fdata_frame[f].q[2];
                 const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
                 if (Wm == 0.0f) continue;
                 const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);

@@ -116,7 +116,7 @@ __device__ __forceinline__ uint32_t key_low(uint64_t best) { return NoDepth ? 0x
 template <bool NoDepth>
 __device__ __forceinline__ void depth_update(const Rec &r, uint32_t key, float fxl, float fyl, bool in, uint64_t &best)
 {
-    const float zw = depth_at(r.za, r.zb, r.z0, fxl - r.fx0, fyl - r.fy0);
+    const float zw = depth_at(r.za, r.zb, r.z0, fxl - rec_fx0(r.X0), fyl - rec_fx0(r.Y0));
     const float zc = __builtin_amdgcn_fmed3f(zw, 0.0f, 1.0f);
     const uint64_t k = depth_key<NoDepth>(depth_q24(zc), key);
     const bool win = in && zc == zw && k < best;
@@ -130,7 +130,7 @@ __device__ __noinline__ uint32_t large_block_mask(const Rec *rp, int32_t px0, in
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int64_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
-        const int64_t e0 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
+        const int64_t e0 = (int64_t)R.A[k] * (int64_t)(px0 - R.X0) + ((int64_t)R.B[k] * (int64_t)(py0 - R.Y0) + (k == 0 ? R.D : 0)) + owned;
         const int64_t a = (int64_t)R.A[k] * 256, bb = (int64_t)R.B[k] * 256;
         // over a wave's rectangle [ox, ox + kWaveW) x [oy, oy + kWaveH): max of E at its origin + the
         // positive parts of the steps across it
@@ -171,7 +171,8 @@ __device__ __forceinline__ uint32_t stage_tile(const Rec *__restrict__ frame_rec
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int32_t owned = (R.A[k] > 0 || (R.A[k] == 0 && R.B[k] < 0)) ? 1 : 0;
-        const int64_t e64 = (int64_t)R.A[k] * (int64_t)px0 + ((int64_t)R.B[k] * (int64_t)py0 + R.C[k]) + owned;
+        const int64_t e64 =
+            (int64_t)R.A[k] * (int64_t)(px0 - R.X0) + ((int64_t)R.B[k] * (int64_t)(py0 - R.Y0) + (k == 0 ? R.D : 0)) + owned;
         const int32_t e0 = e64 > (1 << 30) ? (1 << 30) : e64 < -(1 << 30) ? -(1 << 30) : (int32_t)e64;
         // (wrapping uint32 arithmetic: a large record's values may wrap here -- its mask is redone below
         // and its edge values are unused -- a small record's never do)
@@ -190,7 +191,7 @@ __device__ __forceinline__ uint32_t stage_tile(const Rec *__restrict__ frame_rec
         E.e[0] = ri;
         E.ab[0] = kLargeAB;
     }
-    E.za = R.za; E.zb = R.zb; E.z0 = R.z0; E.fx0 = R.fx0; E.fy0 = R.fy0;
+    E.za = R.za; E.zb = R.zb; E.z0 = R.z0; E.fx0 = rec_fx0(R.X0); E.fy0 = rec_fx0(R.Y0);
     E.key = rec_key(ri, F);
     large = !small;
     return mask;
@@ -760,7 +761,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         const float3 w = i64x3_to_f32(E[0], E[1], E[2]);
         fE[0] = w.x; fE[1] = w.y; fE[2] = w.z;
     }
-    parent_lambda_f(r, fE, fd.clipped == 0, lam);
+    // 1/w: the FaceData's of a non-clipped face (its record's second half is never written), the record's
+    // own of a clipped sub-triangle
+    float iwv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) iwv[k] = fd.clipped ? r.iw[k] : fd.q[k];
+    parent_lambda_f(r, iwv, fE, fd.clipped == 0, lam);
     if constexpr (GB) {
         if (gbo.depth) gbo.depth[o] = (float)(uint32_t)(best >> 32) / 16777215.0f;
         if (gbo.bary) {

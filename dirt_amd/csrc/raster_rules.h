@@ -22,42 +22,57 @@ constexpr uint32_t kDepthMax = 16777215u;  // 2^24-1 == cleared depth 1.0 (raste
 constexpr int32_t kGbufMulti = 1 << 30;
 constexpr int32_t kGbufIndexMask = kGbufMulti - 1;
 
-// Per (sub-)triangle setup record, 128 B.  The first 80 B are what the tile raster stages in LDS.
+// Per (sub-)triangle setup record, 128 B in two 64-B halves.  The first half is everything the tile raster
+// stages and every coverage test reads (edge functions relative to vertex 0, bbox, depth plane), so a
+// non-clipped face's record is written and read as one 64-B piece; the second half (1/w of the three
+// sub-vertices, parent barycentric basis) is written and read for clipped faces only -- a non-clipped
+// face's 1/w travels in its FaceData (below) and its basis is the identity.
+//   E_k(px, py) = A_k (px - X0) + B_k (py - Y0) + (k == 0 ? D : 0)
+// equals the usual A_k px + B_k py + C_k exactly (vertex 0 lies on edges 1 and 2, and E_0 there is D).
 struct alignas(16) Rec {
     int32_t A[3];
     int32_t B[3];
-    int64_t C[3];
+    int32_t X0, Y0;           // snapped vertex 0 (1/256 px)
+    int64_t D;                // E_0 at vertex 0 = E_0 + E_1 + E_2 everywhere (twice the signed area, > 0)
     uint16_t i0, i1, j0, j1;  // inclusive pixel bbox (window coords, j from the bottom); empty if i0 > i1
+    float z0, za, zb;         // depth plane relative to vertex 0 (R4); fx0, fy0 = X0, Y0 / 256 exactly
     int32_t face;
-    float fx0, fy0, z0, za, zb;  // depth plane relative to snapped vertex 0 (R4)
-    float iw[3];                 // 1/w of the three (sub-)vertices
-    float basis[9];              // row k = parent barycentric of sub-vertex k (identity on the fast path)
+    // second half: clipped records only
+    float iw[3];              // 1/w of the three (sub-)vertices
+    float basis[9];           // row k = parent barycentric of sub-vertex k (identity on the fast path)
+    int32_t pad[4];
 };
 static_assert(sizeof(Rec) == 128, "Rec must be 128 B");
 
-struct alignas(8) EdgePart {  // first 56 B of Rec: what a coverage test needs
+struct alignas(8) EdgePart {  // first 48 B of Rec: what a coverage test needs
     int32_t A[3];
     int32_t B[3];
-    int64_t C[3];
+    int32_t X0, Y0;
+    int64_t D;
     uint16_t i0, i1, j0, j1;
 };
-static_assert(sizeof(EdgePart) == 56, "EdgePart must be 56 B");
+static_assert(sizeof(EdgePart) == 48, "EdgePart must be 48 B");
 
-struct alignas(16) RasterPart {  // first 80 B of Rec
+struct alignas(16) RasterPart {  // first 64 B of Rec
     int32_t A[3];
     int32_t B[3];
-    int64_t C[3];
+    int32_t X0, Y0;
+    int64_t D;
     uint16_t i0, i1, j0, j1;
+    float z0, za, zb;
     int32_t face;
-    float fx0, fy0, z0, za, zb;
 };
-static_assert(sizeof(RasterPart) == 80, "RasterPart must be 80 B");
+static_assert(sizeof(RasterPart) == 64, "RasterPart must be 64 B");
+constexpr int kRecBboxOffset = 40;  // offsetof(Rec, i0): the packed bbox as one 8-B load
+
+__host__ __device__ inline float rec_fx0(int32_t X0) { return (float)X0 * 0.00390625f; }  // exact: |X0| < 2^23
 
 // Per-face data written by setup, read by the resolve and the backward (one 32-B load instead of a
 // faces[] -> vertices[] dependent chain).
 struct alignas(16) FaceData {
     int32_t v[3];  // vertex indices (frame-local)
-    float w[3];    // clip w of the three parent vertices
+    float q[3];    // non-clipped face: 1/w of its three vertices (its record's interpolation data);
+                   // clipped face: clip w of the three parent vertices
     int32_t nsub;     // number of (sub-)triangle records, 0 = culled
     int32_t clipped;  // 1 if set up by the R5 clipping path
 };
@@ -85,18 +100,15 @@ __device__ inline void set_empty(Rec &r, int face)
     r.face = face;
 }
 
-// Store a non-clipped face's record without its basis (bytes 92..127; identity, never read for such faces:
-// parent_lambda_f / fast_lambda take the identity branch from FaceData.clipped / the g-buffer's multi bit)
+// Store a non-clipped face's record: its first 64 B only (the second half -- 1/w, identity basis -- is
+// never read for such faces: the 1/w are in its FaceData, and every basis use takes the identity branch from
+// FaceData.clipped / the g-buffer's multi bit)
 __device__ __forceinline__ void store_record_fast(Rec *dst, const Rec &r)
 {
-    static_assert(offsetof(Rec, basis) == 92, "Rec layout");
     const int4 *s4 = reinterpret_cast<const int4 *>(&r);
     int4 *d4 = reinterpret_cast<int4 *>(dst);
 #pragma unroll
-    for (int k = 0; k < 5; ++k) d4[k] = s4[k];
-    const int *s1 = reinterpret_cast<const int *>(&r) + 20;
-    int *d1 = reinterpret_cast<int *>(dst) + 20;
-    *reinterpret_cast<int3 *>(d1) = *reinterpret_cast<const int3 *>(s1);
+    for (int k = 0; k < 4; ++k) d4[k] = s4[k];
 }
 
 // R1..R4 for one (sub-)triangle: fills `out` (a register-resident local), returns true if non-empty.
@@ -118,20 +130,20 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
     // |X|, |Y| < 2^23 (guard band 16384 px beyond the frame centre, 256 sub-pixels): A, B < 2^24 fit int32
     // and every product is one 32 x 32 -> 64-bit multiply-add (no 64 x 64 multiplies)
     int32_t A[3], B[3];
-    int64_t C[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int a = (k + 1) % 3, b = (k + 2) % 3;
         A[k] = Y[a] - Y[b];
         B[k] = X[b] - X[a];
-        C[k] = -((int64_t)A[k] * X[a] + (int64_t)B[k] * Y[a]);
     }
-    const int64_t D = (int64_t)A[0] * X[0] + (int64_t)B[0] * Y[0] + C[0];
+    // D = E_0 at vertex 0 = A_0 (X0 - X1) + B_0 (Y0 - Y1) (edge 0 runs through vertex 1)
+    int64_t D = (int64_t)A[0] * (X[0] - X[1]) + (int64_t)B[0] * (Y[0] - Y[1]);
     // (no early exits: the emptiness tests select at the end, so the divisions below can start while the
     // integer path is still running -- setup runs one wave per SIMD, where only ILP hides latency)
     const bool neg = D < 0;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { A[k] = neg ? -A[k] : A[k]; B[k] = neg ? -B[k] : B[k]; C[k] = neg ? -C[k] : C[k]; }
+    for (int k = 0; k < 3; ++k) { A[k] = neg ? -A[k] : A[k]; B[k] = neg ? -B[k] : B[k]; }
+    const int64_t Dn = neg ? -D : D;
     int32_t xmin = min(X[0], min(X[1], X[2])), xmax = max(X[0], max(X[1], X[2]));
     int32_t ymin = min(Y[0], min(Y[1], Y[2])), ymax = max(Y[0], max(Y[1], Y[2]));
     int32_t i0 = (xmin - 128 + 255) >> 8, i1 = (xmax - 128) >> 8;  // arithmetic shift = floor
@@ -141,7 +153,7 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
     i1 = i1 > W - 1 ? W - 1 : i1;
     j1 = j1 > H - 1 ? H - 1 : j1;
     const bool nonempty = D != 0 && i0 <= i1 && j0 <= j1;
-    const float fx0 = (float)X[0] * 0.00390625f, fy0 = (float)Y[0] * 0.00390625f;
+    const float fx0 = rec_fx0(X[0]), fy0 = rec_fx0(Y[0]);
     const float dx1 = (float)X[1] * 0.00390625f - fx0, dy1 = (float)Y[1] * 0.00390625f - fy0;
     const float dx2 = (float)X[2] * 0.00390625f - fx0, dy2 = (float)Y[2] * 0.00390625f - fy0;
     const float dz1 = zw[1] - zw[0], dz2 = zw[2] - zw[0];
@@ -153,10 +165,11 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
         fD = (float)D;
     const float det = fD * (1.0f / 65536.0f);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { out.A[k] = A[k]; out.B[k] = B[k]; out.C[k] = C[k]; }
+    for (int k = 0; k < 3; ++k) { out.A[k] = A[k]; out.B[k] = B[k]; }
+    out.X0 = X[0]; out.Y0 = Y[0]; out.D = Dn;
     out.i0 = (uint16_t)i0; out.i1 = (uint16_t)i1; out.j0 = (uint16_t)j0; out.j1 = (uint16_t)j1;
     out.face = face;
-    out.fx0 = fx0; out.fy0 = fy0; out.z0 = zw[0];
+    out.z0 = zw[0];
     out.za = (dz1 * dy2 - dz2 * dy1) / det;
     out.zb = (dx1 * dz2 - dx2 * dz1) / det;
 #pragma unroll
@@ -171,12 +184,14 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
 
 // R3: exact edge values at pixel centre (i,j)
 // (32 x 32 -> 64-bit signed multiplies: one v_mad_i64_i32 each; pixel coordinates fit in 22 bits)
+// (relative to vertex 0: |px - X0|, |py - Y0| < 2^24, so the offsets are int32 and each product is one
+// 32 x 32 -> 64-bit multiply-add)
 template <typename R>
 __device__ __forceinline__ void edge_values(const R &r, int i, int j, int64_t E[3])
 {
-    const int32_t px = i * 256 + 128, py = j * 256 + 128;
+    const int32_t dx = i * 256 + 128 - r.X0, dy = j * 256 + 128 - r.Y0;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) E[k] = (int64_t)r.A[k] * (int64_t)px + ((int64_t)r.B[k] * (int64_t)py + r.C[k]);
+    for (int k = 0; k < 3; ++k) E[k] = (int64_t)r.A[k] * (int64_t)dx + ((int64_t)r.B[k] * (int64_t)dy + (k == 0 ? r.D : 0));
 }
 
 // R3 top-left rule: E > 0, or E == 0 on an owned (left or top) edge  <=>  E + owned > 0
@@ -206,7 +221,7 @@ template <typename R>
 __device__ __forceinline__ bool sample_depth(const R &r, int i, int j, uint32_t &d)
 {
     const float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
-    const float zw = depth_at(r.za, r.zb, r.z0, fx - r.fx0, fy - r.fy0);
+    const float zw = depth_at(r.za, r.zb, r.z0, fx - rec_fx0(r.X0), fy - rec_fx0(r.Y0));
     if (!(zw >= 0.0f && zw <= 1.0f)) return false;
     const uint32_t q = depth_q24(zw);
     if (q >= kDepthMax) return false;
@@ -214,11 +229,13 @@ __device__ __forceinline__ bool sample_depth(const R &r, int i, int j, uint32_t 
     return true;
 }
 
-// R6 from the edge values already converted to float (fE[k] == (float)E[k]); `identity`: the record's
-// basis is the identity (non-clipped face), where (m0*1 + m1*0) + m2*0 == m0 exactly since m_k >= +0
-__device__ __forceinline__ bool parent_lambda_f(const Rec &r, const float fE[3], bool identity, float lam[3])
+// R6 from the edge values already converted to float (fE[k] == (float)E[k]) and the record's 1/w (`iw`:
+// FaceData.q of a non-clipped face, Rec.iw of a clipped one); `identity`: the record's basis is the identity
+// (non-clipped face), where (m0*1 + m1*0) + m2*0 == m0 exactly since m_k >= +0
+__device__ __forceinline__ bool parent_lambda_f(const Rec &r, const float iw[3], const float fE[3], bool identity,
+                                                float lam[3])
 {
-    const float a0 = fE[0] * r.iw[0], a1 = fE[1] * r.iw[1], a2 = fE[2] * r.iw[2];
+    const float a0 = fE[0] * iw[0], a1 = fE[1] * iw[1], a2 = fE[2] * iw[2];
     const float s = (a0 + a1) + a2;
     if (s == 0.0f) return false;
     const float rs = 1.0f / s;

@@ -92,7 +92,7 @@ __device__ __forceinline__ FaceData setup_face_into(const float *vb, const int32
     for (int k = 0; k < 3; ++k) ok = ok && finite4(tri.v[k]);
     FaceData fd;
     fd.v[0] = vidx[0]; fd.v[1] = vidx[1]; fd.v[2] = vidx[2];
-    fd.w[0] = tri.v[0][3]; fd.w[1] = tri.v[1][3]; fd.w[2] = tri.v[2][3];
+    fd.q[0] = tri.v[0][3]; fd.q[1] = tri.v[1][3]; fd.q[2] = tri.v[2][3];
     fd.clipped = 0;
     bool fast = ok;
 #pragma unroll
@@ -107,6 +107,7 @@ __device__ __forceinline__ FaceData setup_face_into(const float *vb, const int32
         const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
         make_record(tri.v, id, W, H, f, r);
         frame_recs[f] = r;
+        fd.q[0] = r.iw[0]; fd.q[1] = r.iw[1]; fd.q[2] = r.iw[2];
         nsub = 1;
     } else {
         frame_recs[f] = r;  // empty unless clip_face overwrites it
@@ -130,7 +131,7 @@ __device__ __forceinline__ void coarse_range(uint32_t bx, uint32_t by, int cshif
 
 __device__ __forceinline__ void load_bbox(const Rec &r, uint32_t &bx, uint32_t &by)
 {
-    const uint2 q = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(&r) + 48);
+    const uint2 q = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(&r) + kRecBboxOffset);
     // Rec stores i0, i1, j0, j1 as consecutive uint16
     bx = q.x;
     by = q.y;
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
                                                             uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
                                                             uint2 *__restrict__ bins, uint32_t slab, int B,
-                                                            const ZeroFill zf)
+                                                            const ZeroFill zf, const float gx, const float gy)
 {
     // workgroups past the faces zero-fill the caller's gradient accumulators (DIRT_FWD zero_grad_*): the
     // setup grid leaves most CUs idle (196 workgroups at config 3), so the fill costs the raster nothing
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     auto count = [&](int32_t, uint32_t, uint32_t, int cx, int cy) { atomicAdd(&hist[cy * nctx + cx], 1u); };
     Rec *frame_recs = recs + (int64_t)b * nrec;
     const float *vb = verts + (int64_t)b * V * 4;
-    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
+    // (guard band gx = 32768 / W, gy = 32768 / H: IEEE divisions on the host, the same floats -- two
+    // correctly rounded division sequences fewer in the one-wave-per-SIMD chain)
     const int f = blockIdx.x * kFacesPerBlock + t;
     // what the placement pass needs again: the fast-path record's packed bbox, or the sub-record count
     int nsub = 0;
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         if (!(i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V)) atomicOr(flag, 1u);
         FaceData fd;
         fd.v[0] = i0; fd.v[1] = i1; fd.v[2] = i2;
-        fd.w[0] = tri.v[0][3]; fd.w[1] = tri.v[1][3]; fd.w[2] = tri.v[2][3];
+        fd.q[0] = tri.v[0][3]; fd.q[1] = tri.v[1][3]; fd.q[2] = tri.v[2][3];  // clip w (clipped faces)
         fd.clipped = 0;
         Rec r;
         set_empty(r, f);
@@ -350,9 +352,10 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
                 make_record(tri.v, id, W, H, f, r);
             }
             nsub = 1;
-            // (the first 92 B: a fast-path record's basis is the identity, and every reader skips it for
-            // non-clipped faces -- 28 % fewer dirty bytes to write back when the kernel ends)
+            // (the record's first 64 B; its 1/w go with the FaceData: one 64-B piece per record instead of
+            // two to write back when the kernel ends and for the raster to fetch)
             store_record_fast(&frame_recs[f], r);
+            fd.q[0] = r.iw[0]; fd.q[1] = r.iw[1]; fd.q[2] = r.iw[2];
             fbx = (uint32_t)r.i0 | ((uint32_t)r.i1 << 16);
             fby = (uint32_t)r.j0 | ((uint32_t)r.j1 << 16);
             coarse_pairs_add(Q, f, fbx, fby, cshift, count);
@@ -435,6 +438,8 @@ void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int
     const int64_t z4 = (zf.na + zf.nb + 3) / 4, want = std::min<int64_t>((z4 + 4095) / 4096, 64);
     const int nzb = z4 > 0 ? (int)std::max<int64_t>(1, (want + B - 1) / B) : 0;
     const dim3 grid((unsigned)(zf.nfb + nzb), (unsigned)B);
+    const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
     setup_kernel<AB><<<grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse,
-                                                             L.nrec, recs, fdata, ccount, flag, bins, L.slab, B, zf);
+                                                             L.nrec, recs, fdata, ccount, flag, bins, L.slab, B, zf, gx,
+                                                             gy);
 }

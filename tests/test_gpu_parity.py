@@ -541,6 +541,27 @@ def test_dense_tiles_slot_table_and_tail_overflow(C, r):
     check_scene(bg, v, c, f)
 
 
+@pytest.mark.parametrize("C", [3, 7])
+def test_dense_tiles_with_clipped_faces(C):
+    """Clipped faces (records carrying their own 1/w and basis in the record's second half) visible in tiles
+    whose distinct records overflow the backward's slot table: their 1/w are then read from the record
+    (grad_kernel.h phase B), and from FaceData.q for the non-clipped ones around them."""
+    bg, v1, c1, f1 = scenes.random_triangles(F=20000, W=64, H=48, C=C, radius_px=0.8, seed=40 + C)
+    _, v2, c2, f2 = scenes.clipping_scene(W=64, H=48, C=C, seed=7)
+    v2 = v2.copy()
+    v2[:, 2] = np.where(v2[:, 3] > 0, 0.97 * v2[:, 3], v2[:, 2])  # far, so the dense layer stays visible
+    v = np.concatenate([v1, v2], 0)
+    c = np.concatenate([c1, c2], 0)
+    f = np.concatenate([f1, f2 + len(v1)], 0).astype(np.int32)
+    _, gb, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
+    g = gb[0]
+    over = [(y, x) for y in range(0, 48, 16) for x in range(0, 64, 16)
+            if len(np.unique(g[y:y + 16, x:x + 16][g[y:y + 16, x:x + 16] >= 0])) > 64]
+    assert over
+    assert any(((g[y:y + 16, x:x + 16] >= 0) & ((g[y:y + 16, x:x + 16] & (1 << 30)) != 0)).any() for y, x in over)
+    check_scene(bg, v, c, f)
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_fused_small_scene_forward(seed):
     """Frames of at most 32 faces take the fused forward (raster_kernel FUSED: each workgroup sets up the
