@@ -74,6 +74,11 @@ constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per wave and c
 // v_dot2_i32_i16 of the packed (A, B) with the lane's packed (dx, dy) offsets (<= 15*256, 3*256).
 constexpr int kDotEdge = 1 << 15;
 constexpr uint32_t kLargeAB = 0x80008000u;  // ab[0] of a large entry (A = B = -2^15 never occurs in a small one)
+// the resolve's int32 path: winners with every |A|, |B| < 2^14 (see the resolve)
+constexpr int32_t kResolveSmall = 1 << 14;
+#ifndef DIRT_RASTER_RESOLVE32
+#define DIRT_RASTER_RESOLVE32 1
+#endif
 
 struct alignas(16) StripEntry {  // 48 B of wave-private LDS per staged (sub-)triangle: three ds_read_b128
     int32_t e[3];    // small: E + owned at the strip origin (2^30 when the edge holds over the whole strip);
@@ -324,19 +329,22 @@ __device__ __noinline__ uint32_t neighbour_bits_i64(const EdgePart &r, int64_t E
 // the coverage tests of the backward's pairs, computed once here for every pixel, so the
 // backward reads them (its own face at p: bit d of p; the neighbour's face at p: bit opposite(d) of q)
 // instead of re-testing records per pair.
-__device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64_t E[3], bool multi, int32_t ri,
+__device__ __forceinline__ uint32_t neighbour_coverage(const RasterPart &r, const int64_t E[3], bool multi, int32_t ri,
                                                        const Rec *frame_recs, const FaceData *fdata_frame, int F, int f,
-                                                       int i, int j)
+                                                       int i, int j, bool known_small = false)
 {
     // int32 when every lane's |E| < 2^30 and |A|, |B| < 2^22 (a one-pixel step stays inside int32);
-    // otherwise the out-of-line int64 version (a real branch, not both paths)
+    // otherwise the out-of-line int64 version (a real branch, not both paths).  `known_small` (wave-uniform):
+    // the resolve's int32 path already bounds |E| < 2^30 and |A|, |B| < 2^14
     bool small = true;
+    if (!known_small) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-        small = small && (uint64_t)(E[k] + (1ll << 30)) < (2ull << 30) && (uint32_t)(r.A[k] + (1 << 22)) < (2u << 22) &&
-                (uint32_t)(r.B[k] + (1 << 22)) < (2u << 22);
+        for (int k = 0; k < 3; ++k)
+            small = small && (uint64_t)(E[k] + (1ll << 30)) < (2ull << 30) && (uint32_t)(r.A[k] + (1 << 22)) < (2u << 22) &&
+                    (uint32_t)(r.B[k] + (1 << 22)) < (2u << 22);
+    }
     uint32_t bits = 0;
-    if (__builtin_amdgcn_ballot_w64(!small) == 0) {
+    if (known_small || __builtin_amdgcn_ballot_w64(!small) == 0) {
         int32_t eo[3];  // E + owned
 #pragma unroll
         for (int k = 0; k < 3; ++k) eo[k] = (int32_t)E[k] + ((r.A[k] > 0 || (r.A[k] == 0 && r.B[k] < 0)) ? 1 : 0);
@@ -349,7 +357,8 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const Rec &r, const int64
             bits |= (min(q0, min(q1, q2)) > 0 ? 1u : 0u) << dir;
         }
     } else {
-        bits = neighbour_bits_i64(*reinterpret_cast<const EdgePart *>(&r), E[0], E[1], E[2]);
+        // (the global record, not the caller's register copy: a noinline callee would put that in scratch)
+        bits = neighbour_bits_i64(*reinterpret_cast<const EdgePart *>(&frame_recs[ri]), E[0], E[1], E[2]);
     }
     if (multi) {
 #pragma unroll
@@ -744,22 +753,45 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         return;
     }
     const Rec &r = frame_recs[best_rec];
+    // the record's first 64 B as one batch of loads (four dwordx4 in flight with the FaceData): reading
+    // fields on demand lets the compiler split them into dependent rounds behind the range test below
+    const RasterPart rp = *reinterpret_cast<const RasterPart *>(&r);
     const FaceData fd = fdata_frame[face_of_record(best_rec, F)];
     gbuffer[o] = best_rec | (fd.clipped ? kGbufMulti : 0);
     int64_t E[3];
-    edge_values(r, i, j, E);
     float lam[3] = {0.0f, 0.0f, 0.0f};
-    // R6 with the int64 -> float conversions done in int32 when every value of the wave fits (the same
-    // integers, so the same floats); non-clipped faces skip the identity basis (m_k >= +0 are exact)
-    bool fits = true;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) fits = fits && E[k] == (int64_t)(int32_t)E[k];
     float fE[3];
+    // Small winners (every |A|, |B| < 2^14: edges shorter than 64 px) -- the pixel centre lies inside the
+    // triangle, so |px - X0|, |py - Y0| <= the bbox extent < 2^14 and |D| < 2^29: E = A dx + B dy (+ D) in
+    // int32 with 24-bit multiplies, exact (|E| < 2^30), instead of six 32x32->64 multiply-adds; the same
+    // integers, so the same floats.  Otherwise (a wave-uniform branch) the int64 path below.
+    bool small_rec = true;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) fE[k] = (float)(int32_t)E[k];
-    if (__builtin_amdgcn_ballot_w64(!fits) != 0) {  // (a real branch: the int64 conversions are not inlined)
-        const float3 w = i64x3_to_f32(E[0], E[1], E[2]);
-        fE[0] = w.x; fE[1] = w.y; fE[2] = w.z;
+    for (int k = 0; k < 3; ++k)
+        small_rec = small_rec && (uint32_t)(rp.A[k] + kResolveSmall) < 2u * kResolveSmall &&
+                    (uint32_t)(rp.B[k] + kResolveSmall) < 2u * kResolveSmall;
+    const bool resolve_small = DIRT_RASTER_RESOLVE32 && __builtin_amdgcn_ballot_w64(!small_rec) == 0;
+    if (resolve_small) {
+        const int32_t dx = i * 256 + 128 - rp.X0, dy = j * 256 + 128 - rp.Y0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int32_t e = __mul24(rp.A[k], dx) + __mul24(rp.B[k], dy) + (k == 0 ? (int32_t)rp.D : 0);
+            E[k] = e;
+            fE[k] = (float)e;
+        }
+    } else {
+        edge_values(rp, i, j, E);
+        // R6 with the int64 -> float conversions done in int32 when every value of the wave fits (the same
+        // integers, so the same floats); non-clipped faces skip the identity basis (m_k >= +0 are exact)
+        bool fits = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fits = fits && E[k] == (int64_t)(int32_t)E[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fE[k] = (float)(int32_t)E[k];
+        if (__builtin_amdgcn_ballot_w64(!fits) != 0) {  // (a real branch: the int64 conversions are not inlined)
+            const float3 w = i64x3_to_f32(E[0], E[1], E[2]);
+            fE[0] = w.x; fE[1] = w.y; fE[2] = w.z;
+        }
     }
     // 1/w: the FaceData's of a non-clipped face (its record's second half is never written), the record's
     // own of a clipped sub-triangle
@@ -836,8 +868,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
         }
         covbits[o] = (AB & 32) ? (uint8_t)0
-                               : (uint8_t)neighbour_coverage(r, E, fd.clipped != 0, best_rec, frame_recs,
-                                                             fdata_frame, F, face_of_record(best_rec, F), i, j);
+                               : (uint8_t)neighbour_coverage(rp, E, fd.clipped != 0, best_rec, frame_recs,
+                                                             fdata_frame, F, face_of_record(best_rec, F), i, j,
+                                                             resolve_small);
         PHASE_TS(5);
     }
 }

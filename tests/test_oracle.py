@@ -209,3 +209,26 @@ def test_gbuffer_outputs_consistent():
     _, _, depth, _, face, _ = oracle.rasterise_fwd_gbuffer(*(a[None] for a in scenes.readme_square()))
     assert set(np.unique(face)) == {-1, 0, 1}
     assert np.all(depth[face >= 0] == np.float32(np.float32(8388608) / np.float32(16777215)))
+
+
+@pytest.mark.parametrize("perspective", [False, True])
+@pytest.mark.parametrize("centre_snap", [False, True])
+def test_oracle_coverage_matches_exact_integer_rule(centre_snap, perspective):
+    """The oracle's visible face on watertight meshes equals the exact-integer statement of R1-R3 in
+    tests/exact_cover.py (Python ints, independent of oracle/dirt_oracle.c), and the rule is watertight:
+    every pixel centre strictly inside the mesh lies in exactly one triangle, shared edges and vertices on
+    pixel centres included."""
+    from exact_cover import exact_cover, grid_mesh, snap
+    H, W = 80, 96
+    v, faces = grid_mesh(7, 6, W, H, seed=11 + 2 * centre_snap + perspective, perspective=perspective,
+                         centre_snap=centre_snap)
+    count, first = exact_cover(v, faces, W, H)
+    X, Y = snap(v, W, H)
+    pxc, pyc = np.arange(W) * 256 + 128, (np.arange(H) * 256 + 128)[::-1]
+    strict = ((pxc[None, :] > X.min()) & (pxc[None, :] < X.max())) & ((pyc[:, None] > Y.min()) & (pyc[:, None] < Y.max()))
+    assert count.max() == 1 and np.all(count[strict] == 1)
+    rng = np.random.default_rng(3)
+    bg = rng.uniform(0, 1, (1, H, W, 3)).astype(np.float32)
+    cols = rng.uniform(0, 1, (1, len(v), 3)).astype(np.float32)
+    face = oracle.rasterise_fwd_gbuffer(bg, v[None], cols, faces[None])[4][0]
+    np.testing.assert_array_equal(face, first)
