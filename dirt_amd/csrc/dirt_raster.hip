@@ -490,7 +490,7 @@ int dirt_debug_raster_variant(int variant, const float *background, const float 
                                                              nullptr, 0, nullptr, nullptr, 0, C);                    \
         break
     switch (variant) {
-        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8); V_RAST(32); V_RAST(64); V_RAST(96); V_RAST(128); V_RAST(512);
+        V_RAST(0); V_RAST(1); V_RAST(2); V_RAST(4); V_RAST(8); V_RAST(32); V_RAST(64); V_RAST(96); V_RAST(128); V_RAST(512); V_RAST(1024); V_RAST(2048);
     default:
         return fail(DIRT_EINVAL, "dirt_debug_raster_variant: unknown variant");
     }

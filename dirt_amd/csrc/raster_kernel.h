@@ -374,7 +374,8 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const RasterPart &r, cons
 
 // AB: ablation mask for tools/ablate.py (0 in the product): 1 skip the per-pixel loop, 2 skip
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too,
-// 32 no neighbour-coverage bits, 64 no colour loads (lambda written), 128 phase timestamps
+// 32 no neighbour-coverage bits, 64 no colour loads (lambda written), 128 phase timestamps, 512 / 1024 / 2048 one
+// extra dependent global round trip before the slab loads / before the colour loads / before the record loads
 #ifndef DIRT_RASTER_WAVES
 #define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
                              // the procedural programs and the generic-C path keep their natural allocation)
@@ -752,7 +753,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         PHASE_TS(5);
         return;
     }
-    const Rec &r = frame_recs[best_rec];
+    int32_t best_q = best_rec;
+    if (AB & 2048) {
+        // ablation: one extra dependent global round trip between the depth resolve and the record loads
+        uint32_t z0, z1;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z0) : "v"(best_rec));
+        const uint32_t w = flag[kParQ + z0];
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z1) : "v"(w));
+        best_q += (int32_t)z1;
+    }
+    const Rec &r = frame_recs[best_q];
     // the record's first 64 B as one batch of loads (four dwordx4 in flight with the FaceData): reading
     // fields on demand lets the compiler split them into dependent rounds behind the range test below
     const RasterPart rp = *reinterpret_cast<const RasterPart *>(&r);
@@ -864,6 +874,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             for (int k = 0; k < C; ++k) out[k] = lam[k % 3];
         } else {
             const float *cb = colors + (int64_t)b * V * C;
+            if (AB & 1024) {
+                // ablation: one extra dependent global round trip between the FaceData and the colour loads
+                uint32_t z0, z1;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z0) : "v"(fd.v[0]));
+                const uint32_t w = flag[kParQ + z0];
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z1) : "v"(w));
+                cb += z1;
+            }
             const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
             for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
         }

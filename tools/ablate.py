@@ -59,7 +59,8 @@ def main():
     RN = {0: "full", 1: "no pixel loop, no resolve", 2: "bin filter only, no resolve", 4: "no resolve",
           8: "nothing (housekeeping + bg prefetch + gbuffer write)", 32: "no coverage bits",
           64: "no colour loads", 96: "no coverage bits, no colour loads",
-          512: "one extra round trip before the slab loads"}
+          512: "one extra round trip before the slab loads", 1024: "one extra round trip before the colour loads",
+          2048: "one extra round trip before the record loads"}
     rres = {k: [] for k in RN}
     for rnd in range(30):
         for k in RN:
