@@ -1314,26 +1314,41 @@ static int covers_face(const orc_rec *recs, const int32_t *nsub, int F, int f, i
     return 0;
 }
 
-/* owner h (record r), pair midpoint between samples (i,j) and (i2,j2), axis 0=x 1=y */
+/* owner h (record r), pair midpoint between samples (i,j) and (i2,j2), axis 0=x 1=y.
+ * `identity`: the record belongs to a face that did not take the clipping path (identity basis, its 1/w the
+ * face's own): then lambda_k / Wm = a_k / sum_k (a_k w_k) = a_k / sum_k E_k with a_k = E_k / w_k, and the edge
+ * functions at the pair midpoint sum to 2D exactly (E_0 + E_1 + E_2 = D at every sample), so the weight needs
+ * no normalisation.  Normalising first (lambda = a / sum a, Wm = sum lambda w) cancels catastrophically on
+ * slivers, where the E_k are ~10^3 x D: the fuzz scene of seed 37851 (a 1811-unit sliver) lost 4e-4 relative
+ * that way against a float64 evaluation, which the HIP backward (the same exact-2D form) matched to 1e-6. */
 static void add_pair_owner(const orc_rec *r, const float *vb, const int32_t *fb, int W, int H,
-                           int i, int j, int i2, int j2, int axis, float s, float omega, double *gv)
+                           int i, int j, int i2, int j2, int axis, float s, float omega, int identity, double *gv)
 {
     int64_t E1[3], E2[3], E[3];
     edge_values(r, i, j, E1);
     edge_values(r, i2, j2, E2);
     for (int k = 0; k < 3; ++k) E[k] = E1[k] + E2[k];
-    float lam[3];
-    if (!parent_lambda(r, E, lam)) return;
     const int32_t *f3 = fb + 3 * (int64_t)r->face;
-    float w0 = vb[(int64_t)f3[0] * 4 + 3], w1 = vb[(int64_t)f3[1] * 4 + 3], w2 = vb[(int64_t)f3[2] * 4 + 3];
-    float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
-    if (Wm == 0.0f) return;
     float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
     float mid = axis == 0 ? (float)(i + 1) : (float)(j + 1);
     float ndc = mid / half - 1.0f;
-    float t = ((omega * s) * half) / Wm;
+    float g3[3];
+    if (identity) {
+        const int64_t twoD = E[0] + E[1] + E[2];
+        if (twoD == 0) return;
+        const float t = ((omega * s) * half) / (float)twoD;
+        for (int k = 0; k < 3; ++k) g3[k] = t * ((float)E[k] * r->iw[k]);
+    } else {
+        float lam[3];
+        if (!parent_lambda(r, E, lam)) return;
+        float w0 = vb[(int64_t)f3[0] * 4 + 3], w1 = vb[(int64_t)f3[1] * 4 + 3], w2 = vb[(int64_t)f3[2] * 4 + 3];
+        float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
+        if (Wm == 0.0f) return;
+        float t = ((omega * s) * half) / Wm;
+        for (int k = 0; k < 3; ++k) g3[k] = t * lam[k];
+    }
     for (int k = 0; k < 3; ++k) {
-        float g = t * lam[k];
+        float g = g3[k];
         double *d = gv + (int64_t)f3[k] * 4;
         d[axis] += (double)g;
         d[3] += (double)(-(g * ndc));
@@ -1359,6 +1374,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
     int status = 0;
     orc_rec *recs = (orc_rec *)malloc(sizeof(orc_rec) * 6 * (size_t)(F > 0 ? F : 1));
     int32_t *nsub = (int32_t *)malloc(sizeof(int32_t) * (size_t)(F > 0 ? F : 1));
+    int32_t *clipped = (int32_t *)malloc(sizeof(int32_t) * (size_t)(F > 0 ? F : 1));
     int nthr = 1;
 #ifdef _OPENMP
     nthr = omp_get_max_threads();
@@ -1368,7 +1384,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
     for (int b = 0; b < B; ++b) {
         const float *vb = vertices + (int64_t)b * V * 4;
         const int32_t *fb = faces + (int64_t)b * F * 3;
-        if (setup_frame(vb, fb, V, F, W, H, recs, nsub, NULL)) status = 2;
+        if (setup_frame(vb, fb, V, F, W, H, recs, nsub, clipped)) status = 2;
         memset(accv, 0, sizeof(double) * (size_t)nthr * V * 4);
         memset(accc, 0, sizeof(double) * (size_t)nthr * V * C);
 #pragma omp parallel
@@ -1417,20 +1433,21 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
                         float s = -0.5f * acc;
                         if (s == 0.0f) continue;
                         int fp = rp >= 0 ? recs[rp].face : -1, fq = rq >= 0 ? recs[rq].face : -1;
+                        const int idp = fp >= 0 && !clipped[fp], idq = fq >= 0 && !clipped[fq];
                         if (fp == fq || fq < 0) {
-                            add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                            add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, idp, gv);
                         } else if (fp < 0) {
-                            add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                            add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, idq, gv);
                         } else {
                             int cfq = covers_face(recs, nsub, F, fp, i2, j2);
                             int cgp = covers_face(recs, nsub, F, fq, i, j);
                             if (!cfq && cgp) {
-                                add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                                add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, idp, gv);
                             } else if (cfq && !cgp) {
-                                add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, gv);
+                                add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 1.0f, idq, gv);
                             } else {
-                                add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gv);
-                                add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, gv);
+                                add_pair_owner(&recs[rp], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, idp, gv);
+                                add_pair_owner(&recs[rq], vb, fb, W, H, i, j, i2, j2, axis, s, 0.5f, idq, gv);
                             }
                         }
                     }
@@ -1448,7 +1465,7 @@ int oracle_rasterise_bwd(const float *vertices, const float *vertex_colors, cons
             grad_vertex_colors[(int64_t)b * V * C + v] = (float)a;
         }
     }
-    free(recs); free(nsub); free(accv); free(accc);
+    free(recs); free(nsub); free(clipped); free(accv); free(accc);
     return status;
 }
 
