@@ -348,12 +348,14 @@ def test_deep_depth_complexity_culling(perspective):
     check_scene(bg, v2, c2, f2)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUZZ_SEEDS", "36"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_FUZZ_SEEDS", "36"))))
 def test_fuzz_adversarial_scenes(seed):
     """Raster-rule edge cases mixed at random (scenes.adversarial_scene): pixel-centre / pixel-edge
     vertices, slivers, sub-pixel triangles, duplicate and coplanar faces, near / far / w <= 0 clipping,
-    guard-band overflow; three frame shapes, one batch of two.  DIRT_FUZZ_SEEDS=N runs N seeds (the
-    default suite runs 36); seeds past 36 also cycle the channel count over 3, 7, 1, 5."""
+    guard-band overflow; three frame shapes, one batch of two.  DIRT_FUZZ_SEEDS=N runs seeds below N (the
+    default suite runs 36), from DIRT_FUZZ_FIRST (default 0); seeds past 36 also cycle the channel count
+    over 3, 7, 1, 5."""
     W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
     C = 3 if seed < 36 else (3, 7, 1, 5)[seed % 4]
     if seed % 4 == 3:
