@@ -116,12 +116,10 @@ struct Layout {
 };
 
 constexpr int kMaxCoarse = 4096;   // LDS histogram size in setup
-constexpr int kFacesPerThread = 1;
 #ifndef DIRT_BIN_THREADS
 #define DIRT_BIN_THREADS 256
 #endif
 constexpr int kBinThreads = DIRT_BIN_THREADS;
-constexpr int kFacesPerBlock = kFacesPerThread * kBinThreads;
 constexpr int64_t kDefaultBinBudget = 1ll << 27;  // entries (1 GiB) above which the default slab shrinks
 // Count-set parity, so that no kernel has to return the counts it read to zero.  Words of the flag area
 // (separate 64-B lines): [0] out-of-range-face flag, [kParP] P, [kParQ] Q.  The setup kernel reads p = Q,

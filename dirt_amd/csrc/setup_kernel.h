@@ -250,8 +250,8 @@ struct ZeroFill {
 // K1: setup + coarse binning.  Bin entry = {record index, bbox clamped to the coarse tile, 8 bits per
 // side}; order inside a slab is irrelevant (the depth resolve is a commutative min).
 // AB & 128: per-workgroup phase timestamps (dirt_debug_setup_ts, tools/setup_ts.py)
-template <int AB = 0>
-__global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restrict__ verts,
+template <int AB = 0, int NT = kBinThreads>
+__global__ __launch_bounds__(NT) void setup_kernel(const float *__restrict__ verts,
                                                             const int32_t *__restrict__ faces, int V, int F, int W,
                                                             int H, int cshift, int nctx, int ncoarse, int64_t nrec,
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
@@ -278,9 +278,9 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
         const int64_t g = (int64_t)blockIdx.y * zf.nfb + blockIdx.x, ng = (int64_t)zf.nfb * gridDim.y;  // face workgroups
         if (g == 0 && t == 0) flag[kParP] = par;
         uint32_t *other = counts + (par ^ 1u) * ncount * kCountStride;
-        for (int64_t k = g * kBinThreads + t; k < ncount; k += ng * kBinThreads) other[k * kCountStride] = 0;
+        for (int64_t k = g * NT + t; k < ncount; k += ng * NT) other[k * kCountStride] = 0;
     }
-    for (int c = t; c < ncoarse; c += kBinThreads) hist[c] = 0;
+    for (int c = t; c < ncoarse; c += NT) hist[c] = 0;
     if (t == 0) Q.n = 0;
     __syncthreads();
     auto count = [&](int32_t, uint32_t, uint32_t, int cx, int cy) { atomicAdd(&hist[cy * nctx + cx], 1u); };
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     const float *vb = verts + (int64_t)b * V * 4;
     // (guard band gx = 32768 / W, gy = 32768 / H: IEEE divisions on the host, the same floats -- two
     // correctly rounded division sequences fewer in the one-wave-per-SIMD chain)
-    const int f = blockIdx.x * kFacesPerBlock + t;
+    const int f = blockIdx.x * NT + t;  // (one face per thread)
     // what the placement pass needs again: the fast-path record's packed bbox, or the sub-record count
     int nsub = 0;
     bool fast = false;
@@ -379,12 +379,12 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
     }
     PHASE_TS(1);
     // (the placement pass queues the same records again: with none queued here, it needs no flush)
-    const int nbig = coarse_pairs_flush<kBinThreads>(Q, count);
+    const int nbig = coarse_pairs_flush<NT>(Q, count);
     PHASE_TS(2);
     // reserve this workgroup's range of every touched slab: one returning device atomic per (workgroup,
     // coarse tile), all in flight together
     uint32_t *cc = ccount + (int64_t)b * ncoarse * kCountStride;
-    for (int c = t; c < ncoarse; c += kBinThreads) {
+    for (int c = t; c < ncoarse; c += NT) {
         const uint32_t n = hist[c];
         // (AB & 1: ablation, no reservation; AB & 4: probe, workgroups split over two counters per tile --
         // timing only, the raster would not find the second half)
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kBinThreads) void setup_kernel(const float *__restr
             coarse_pairs_add(Q, (int32_t)ri, bx, by, cshift, place);
         }
     }
-    if (nbig > 0) coarse_pairs_flush<kBinThreads>(Q, place);
+    if (nbig > 0) coarse_pairs_flush<NT>(Q, place);
     if (AB & 128) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -426,20 +426,33 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Setup workgroup size.  256 faces per workgroup keep the slab-reservation atomics few (one per workgroup and
+// touched coarse tile); a batch with fewer than kSetupSmallGrid such workgroups (BASELINE config 4: one frame of
+// 20k faces, 79 workgroups) leaves most CUs idle, and 128-face workgroups there shorten the setup (c4 setup
+// 8.6-10.0 -> 7.6-8.0 us; c3, 196 workgroups, loses 1 us with them: profiles/r03/ab_setup_threads/).
+constexpr int64_t kSetupSmallGrid = 128;
+
 // launch the setup (and binning) of B frames x F faces
 template <int AB = 0>
 void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F, const Layout &L,
                   Rec *recs, FaceData *fdata, uint32_t *ccount, uint32_t *flag, uint2 *bins, hipStream_t stream,
                   float *zero_a = nullptr, int64_t nzero_a = 0, float *zero_b = nullptr, int64_t nzero_b = 0)
 {
-    ZeroFill zf{zero_a, zero_b, zero_a ? nzero_a : 0, zero_b ? nzero_b : 0, (F + kFacesPerBlock - 1) / kFacesPerBlock};
+    const bool small = (int64_t)B * ((F + kBinThreads - 1) / kBinThreads) < kSetupSmallGrid;
+    const int nt = small ? kBinThreads / 2 : kBinThreads;
+    ZeroFill zf{zero_a, zero_b, zero_a ? nzero_a : 0, zero_b ? nzero_b : 0, (F + nt - 1) / nt};
     // filler workgroups per frame row: ~16 float4 stores per thread, at most 64 in all
     // (rounded up: a few accumulator floats in all, fewer than one float4, still need a filler workgroup)
     const int64_t z4 = (zf.na + zf.nb + 3) / 4, want = std::min<int64_t>((z4 + 4095) / 4096, 64);
     const int nzb = z4 > 0 ? (int)std::max<int64_t>(1, (want + B - 1) / B) : 0;
     const dim3 grid((unsigned)(zf.nfb + nzb), (unsigned)B);
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
-    setup_kernel<AB><<<grid, dim3(kBinThreads), 0, stream>>>(vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse,
-                                                             L.nrec, recs, fdata, ccount, flag, bins, L.slab, B, zf, gx,
-                                                             gy);
+    if (small)
+        setup_kernel<AB, kBinThreads / 2><<<grid, dim3(kBinThreads / 2), 0, stream>>>(
+            vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins, L.slab, B,
+            zf, gx, gy);
+    else
+        setup_kernel<AB, kBinThreads><<<grid, dim3(kBinThreads), 0, stream>>>(
+            vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins, L.slab, B,
+            zf, gx, gy);
 }
