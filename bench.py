@@ -270,6 +270,34 @@ def main():
 
     kern_us = kernel_times(step, args.profile_steps)
     kbytes, fwd_b, bwd_b = alg_bytes(B, H, W, C, V, F)
+
+    def pass_times_graph(n=50):
+        """Each pass inside a replayed graph, without the per-launch gap that the event pair around an eager
+        launch includes: HIP events around one replay of n forwards (setup + raster) and of n backwards (grad
+        alone: the backward accumulates, so repeating it is the same work).  rocprofv3 --kernel-trace reports
+        the same durations (profiles/r03/ev2_kernel_stats_graph.csv)."""
+        out = {}
+        for name, fn in (("fwd_setup_plus_raster", lambda: sess.forward(bg, v, c, f)),
+                         ("bwd_grad", lambda: sess.backward(grad))):
+            g = graph_of(fn, n, cap_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()  # (replay() launches on the current stream)
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            out[name] = e0.elapsed_time(e1) * 1e3 / n
+            del g
+        step()  # (the session's buffers hold one consistent forward + backward again)
+        torch.cuda.synchronize()
+        return out
+
+    pass_us = None
+    if not args.no_graph:
+        try:
+            pass_us = pass_times_graph()
+        except Exception as e:  # noqa: BLE001 -- informative field only
+            print("graph pass timing failed: %s" % e, file=sys.stderr)
+            torch.cuda.synchronize()
     dom = max((k for k in kern_us if k in kbytes), key=lambda k: kern_us[k])
     achieved = kbytes[dom] / (kern_us[dom] * 1e-6) / 1e9
     traffic = None
@@ -294,6 +322,15 @@ def main():
         roofline["bwd_frac"] = round(bwd_b / (t_bwd * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     if traffic is not None:
         roofline["traffic_frac"] = round(traffic / (kern_us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    if pass_us:
+        # the same fractions on the passes' in-graph times (no launch gap; the roofline above stays on the
+        # conservative eager event times)
+        roofline["graph_pass_us"] = {k: round(u, 2) for k, u in pass_us.items()}
+        roofline["fwd_frac_graph"] = round(fwd_b / (pass_us["fwd_setup_plus_raster"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        roofline["bwd_frac_graph"] = round(bwd_b / (pass_us["bwd_grad"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        roofline["grad_kernel_frac_graph"] = round(kbytes["grad_kernel"] / (pass_us["bwd_grad"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        if traffic is not None and dom == "grad_kernel":
+            roofline["traffic_frac_graph"] = round(traffic / (pass_us["bwd_grad"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
 
     legs = {}
 
