@@ -36,6 +36,30 @@ def gather_frames(local, batch, group=None):
     return torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
 
 
+def gather_frames_to(local, batch, dst=0, group=None):
+    """Gather per-rank frame blocks into the full batch on rank `dst` only ("ncclGather to rank 0 if
+    only one consumer"); returns the batch on `dst` and None on the other ranks.  Every rank sends its block
+    once (RCCL send / recv over xGMI with the "nccl" backend); the root's ingress bounds it like the
+    all-gather's per-rank ingress, but the other ranks receive nothing."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = [shard_bounds(batch, r, world) for r in range(world)]
+    mx = max(hi - lo for lo, hi in sizes)
+    if local.shape[0] == mx:
+        pad = local.contiguous()
+    else:
+        pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[: local.shape[0]] = local
+    via_host = pad.is_cuda and dist.get_backend(group) == "gloo"  # gloo moves host memory only
+    src = pad.cpu() if via_host else pad
+    outs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+    dist.gather(src, gather_list=outs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    full = torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
+    return full.to(local.device) if via_host else full
+
+
 def gather_frames_async(local, batch, group=None):
     """Start gathering per-rank frame blocks; returns (work, finish) where finish() -> the full batch.
 

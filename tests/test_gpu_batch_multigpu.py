@@ -54,7 +54,8 @@ def _free_port():
 
 def _nccl_worker(port, inputs, outq):
     import torch.distributed as dist
-    from dirt_amd.sharding import gather_frames, gather_frames_async, rasterise_batch_sharded, shared_across_ranks
+    from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, rasterise_batch_sharded,
+                                   shared_across_ranks)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -66,7 +67,8 @@ def _nccl_worker(port, inputs, outq):
         work, finish = gather_frames_async(local, bg.shape[0])
         full2 = finish()
         full3 = rasterise_batch_sharded(bg, v, c, f, gather=True)
-        assert full.is_cuda and full2.is_cuda
+        full4 = gather_frames_to(local, bg.shape[0], dst=0)  # RCCL gather to one root
+        assert full.is_cuda and full2.is_cuda and full4.is_cuda
         # a parameter shared by the rank's frames: all_reduce over RCCL (world 1: the identity)
         x = torch.arange(6, dtype=torch.float32, device=dev).requires_grad_(True)
         (shared_across_ranks(x) * 2.0).sum().backward()
@@ -74,8 +76,8 @@ def _nccl_worker(port, inputs, outq):
         y = torch.ones(1000, device=dev)
         dist.all_reduce(y)
         torch.cuda.synchronize()
-        outq.put((lo, hi, full.cpu().numpy(), full2.cpu().numpy(), full3.cpu().numpy(), x.grad.cpu().numpy(),
-                  float(y.sum())))
+        outq.put((lo, hi, full.cpu().numpy(), full2.cpu().numpy(), full3.cpu().numpy(), full4.cpu().numpy(),
+                  x.grad.cpu().numpy(), float(y.sum())))
     finally:
         dist.destroy_process_group()
 
@@ -97,11 +99,11 @@ def test_rccl_world1_gather_and_allreduce_on_device():
             if not p.is_alive():
                 break
     assert res is not None, "nccl worker exited with %s" % p.exitcode
-    lo, hi, full, full2, full3, xgrad, ysum = res
+    lo, hi, full, full2, full3, full4, xgrad, ysum = res
     p.join(timeout=120)
     assert p.exitcode == 0
     assert (lo, hi) == (0, 3)
-    for a in (full, full2, full3):
+    for a in (full, full2, full3, full4):
         np.testing.assert_array_equal(a, ref)
     np.testing.assert_array_equal(xgrad, np.full(6, 2.0, np.float32))
     assert ysum == 1000.0

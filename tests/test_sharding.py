@@ -14,8 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import scenes
-from dirt_amd.sharding import (gather_frames, gather_frames_async, rasterise_batch_sharded, shard_bounds,
-                               shared_across_ranks)
+from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, rasterise_batch_sharded,
+                               shard_bounds, shared_across_ranks)
 from oracle import oracle
 
 
@@ -55,11 +55,13 @@ def _worker(rank, world, port, inputs, outq):
         full2 = rasterise_batch_sharded(bg, v, c, f, render=_oracle_render, gather=True)
         work, finish = gather_frames_async(local, bg.shape[0])
         full3 = finish()
+        root = gather_frames_to(local, bg.shape[0], dst=1)  # the single-consumer gather: rank 1 only
+        root = None if root is None else root.numpy()
         # a parameter shared by every rank's frames: its gradient is summed over the ranks
         x = torch.arange(6, dtype=torch.float32).requires_grad_(True)
         loss = (shared_across_ranks(x) * (rank + 1)).sum() + (x * x).sum() * 0.0
         loss.backward()
-        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy(), full3.numpy(), x.grad.numpy()))
+        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy(), full3.numpy(), x.grad.numpy(), root))
     finally:
         dist.destroy_process_group()
 
@@ -80,8 +82,12 @@ def test_two_rank_sharded_batch_matches_single_process(B):
         assert p.exitcode == 0
     res.sort(key=lambda r: r[0])
     covered = []
-    for rank, lo, hi, local, full, full2, full3, xgrad in res:
+    for rank, lo, hi, local, full, full2, full3, xgrad, root in res:
         np.testing.assert_array_equal(full3, ref)          # the async all_gather_into_tensor path
+        if rank == 1:
+            np.testing.assert_array_equal(root, ref)       # gather to one root reassembles the batch there
+        else:
+            assert root is None
         np.testing.assert_array_equal(xgrad, np.full(6, 3.0, np.float32))  # (1 + 2) summed over ranks
         assert (lo, hi) == shard_bounds(B, rank, 2)
         np.testing.assert_array_equal(local, ref[lo:hi])   # each rank renders only its frames
