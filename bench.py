@@ -417,6 +417,10 @@ def main():
             gather_frames_async(sess.pixels, batch)[1]()
         n_g = max(10, args.steps // 4)
         t_g = timed(lambda: gather_frames_async(sess.pixels, batch)[1](), n_g, barrier, world, device, shared)
+        # the single-consumer variant: every frame to rank 0 only
+        from dirt_amd.sharding import gather_frames_to
+        gather_frames_to(sess.pixels, batch, dst=0)
+        t_root = timed(lambda: gather_frames_to(sess.pixels, batch, dst=0), n_g, barrier, world, device, shared)
         # pipelined: step k's frames move while step k+1 renders (two sessions, so a frame being gathered
         # is never overwritten; the step that reuses a session first waits for its gather)
         sess2 = RasteriseSession(B, H, W, C, V, F, device=device)
@@ -455,6 +459,7 @@ def main():
             "what": "all_gather_into_tensor of every rank's pixels [%d,%d,%d,%d] over %s per step" %
                     (B, H, W, C, "gloo (shared-GPU rehearsal)" if shared else "RCCL / xGMI"),
             "gather_ms": round(t_g * 1e3 / n_g, 4),
+            "gather_to_rank0_ms": round(t_root * 1e3 / n_g, 4),
             "recv_bytes_per_rank": recv,
             "recv_GBps_per_rank": round(recv / (t_g / n_g) / 1e9, 1),
             "value_with_gather": round(world * B * H * W * args.steps / t_p / 1e6, 1),
