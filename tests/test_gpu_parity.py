@@ -172,6 +172,14 @@ def test_full_size_c3_forward_and_backward():
     check_scene(*scenes.random_triangles(F=50000, W=1024, H=1024, seed=0))
 
 
+@pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("DIRT_FULL_SEEDS", "1"))))
+@pytest.mark.parametrize("perspective", [False, True])
+def test_full_size_c3_more_seeds(seed, perspective):
+    """Config 3's full size on further seeds, affine and perspective (w ~ U(1, 3)); DIRT_FULL_SEEDS=N runs N
+    seeds of each (default 1)."""
+    check_scene(*scenes.random_triangles(F=50000, W=1024, H=1024, seed=seed, perspective=perspective), seed=seed)
+
+
 def test_public_api_single_and_batch():
     import dirt_amd
     bg, v, c, f = scenes.cylinder_scene()
