@@ -18,8 +18,9 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-RTOL = 1e-4
-ATOL_REL = 1e-5
+# (DIRT_GRAD_RTOL / DIRT_GRAD_ATOL_REL override them for measurement campaigns; the suite's contract is these)
+RTOL = float(os.environ.get("DIRT_GRAD_RTOL", "1e-4"))
+ATOL_REL = float(os.environ.get("DIRT_GRAD_ATOL_REL", "1e-5"))
 
 
 def _gpu(a, dtype=None):
