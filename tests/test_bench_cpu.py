@@ -1,0 +1,29 @@
+"""CPU checks of bench.py's bookkeeping (no GPU): the algorithmic byte counts the roofline divides by
+(config 3 forward 29.96 MB, backward 46.75 MB per frame), the frame partition of the N-rank path,
+and the CPU-baseline host description."""
+import bench
+
+
+def test_alg_bytes_match_survey_8d():
+    B, H, W, C, F = 1, 1024, 1024, 3, 50000
+    V = 3 * F
+    k, fwd, bwd = bench.alg_bytes(B, H, W, C, V, F)
+    # fwd = 16V + 12F + 4CV + 4CHW (bg) + 4CHW (pixels); bwd adds grad outputs 16V + 4CV + 4CHW
+    assert fwd == 16 * V + 12 * F + 4 * C * V + 2 * 4 * C * H * W
+    assert bwd == 16 * V + 12 * F + 4 * C * V + 2 * 4 * C * H * W + 16 * V + 4 * C * V + 4 * C * H * W
+    assert abs(fwd / 1e6 - 29.96) < 0.01 and abs(bwd / 1e6 - 46.75) < 0.01  # (SURVEY quotes 2 decimals)
+    # per kernel: the backward's reads + writes (pixels, grad_pixels, grad_background, g-buffer, vertex data)
+    assert k["grad_kernel"] == 3 * 4 * C * H * W + 4 * H * W + 32 * V + 12 * F + 4 * C * V
+    assert k["raster_kernel"] == 2 * 4 * C * H * W + 4 * H * W + 4 * C * V + 12 * F
+    assert k["setup_kernel"] == 12 * F + 16 * V
+    # batches scale linearly
+    k2, fwd2, bwd2 = bench.alg_bytes(8, H, W, C, V, F)
+    assert (fwd2, bwd2) == (8 * fwd, 8 * bwd) and all(k2[n] == 8 * k[n] for n in k)
+
+
+def test_configs_and_host_info():
+    assert bench.CONFIGS["c3"] == (1, 1024, 1024, 3, 50000, 16.0)
+    assert bench.CONFIGS["c5"][0] == 8  # 64 frames over 8 GPUs: 8 per rank
+    info = bench.host_cpu_info()
+    assert set(info) == {"cpu_model", "nproc_online", "affinity_cpus"} and info["affinity_cpus"] >= 1
+    assert bench.cpu_threads() >= 1
