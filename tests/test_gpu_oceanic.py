@@ -1,6 +1,8 @@
 """GPU parity of the `oceanic_horizon` fragment program (shader_id 1): the HIP resolve
 against the CPU oracle, bit for bit (both state the GLSL of csrc/shaders.cpp:1668-1919 in float32 with
 the same fixed sin/cos/pow algorithms, no contraction, IEEE division and sqrt)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -205,6 +207,21 @@ def test_hill_overlap_and_mesh():
     np.testing.assert_array_equal(px, rpx)
     _, v, _, f = scenes.random_triangles(F=400, W=96, H=64, C=3, radius_px=18.0, seed=12, perspective=True)
     T = scenes.hill_terrain(64, 96, 4)[None]
+    px, gb = _hill_gpu(T, v[None], f[None], 3, cam)
+    rpx, rgb, _ = oracle.hill_fwd(T, v[None], f[None], 3, cam)
+    np.testing.assert_array_equal(gb, rgb)
+    np.testing.assert_array_equal(px, rpx)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_HILL_FUZZ_SEEDS", "8"))))
+def test_hill_adversarial_fuzz(seed):
+    """hill (no depth test: the last face in draw order wins) on the adversarial fuzz scenes of
+    tests/test_gpu_parity.py -- pixel-centre vertices, slivers, duplicates, clipping, w <= 0 -- bit-exact
+    g-buffer and pixels.  DIRT_HILL_FUZZ_SEEDS=N widens it (default 8)."""
+    W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
+    _, v, _, f = scenes.adversarial_scene(200000 + seed, W=W, H=H, C=3)
+    T = scenes.hill_terrain(H, W, 4)[None]
+    cam = hill_cam(HILL_CAMS["harness"])
     px, gb = _hill_gpu(T, v[None], f[None], 3, cam)
     rpx, rgb, _ = oracle.hill_fwd(T, v[None], f[None], 3, cam)
     np.testing.assert_array_equal(gb, rgb)
