@@ -213,6 +213,21 @@ def test_hill_overlap_and_mesh():
     np.testing.assert_array_equal(px, rpx)
 
 
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_PROC_FUZZ_SEEDS", "0"))))
+def test_procedural_programs_adversarial_fuzz(seed):
+    """The depth-tested procedural programs (oceanic_horizon and the oceanic family, shader ids 1..6 in turn)
+    on the adversarial fuzz scenes (pixel-centre vertices, slivers, depth ties, clipping, w <= 0): bit-exact
+    g-buffer and pixels.  DIRT_PROC_FUZZ_SEEDS=N runs N scenes (off in the default suite: the CPU oracle of these programs is slow)."""
+    W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
+    sid = 1 + seed % 6
+    bg, v, c, f = (a[None] for a in scenes.adversarial_scene(300000 + seed, W=W, H=H, C=3))
+    cam = np.array(list(CAMS["square_test"]) + [0.3, 0.05, 0.5, 0.0, -0.4, 0.01, 0.0, 0.02], np.float32)
+    px, gb = _family_fwd(sid, bg, v, c, f, cam=cam)
+    rpx, rgb, _ = oracle.rasterise_fwd(bg, v, c, f, shader_id=sid, camera_pos=cam)
+    np.testing.assert_array_equal(gb, rgb)
+    np.testing.assert_array_equal(px, rpx)
+
+
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_HILL_FUZZ_SEEDS", "8"))))
 def test_hill_adversarial_fuzz(seed):
     """hill (no depth test: the last face in draw order wins) on the adversarial fuzz scenes of
