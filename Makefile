@@ -34,7 +34,13 @@ EXT_CXXFLAGS = -O2 -std=c++17 -fPIC -shared -Wall -Wno-unused-function -D__HIP_P
                -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include -I/opt/rocm/include -I$(PY_INC)
 EXT_LDFLAGS = -L$(TORCH_DIR)/lib -ltorch -ltorch_cpu -ltorch_python -lc10 -lc10_hip -Wl,-rpath,$(TORCH_DIR)/lib -ldl
 
+# the C library and the oracle never need torch; the extension is built only where torch imports
+ifeq ($(TORCH_DIR),)
+all: $(LIB) $(ORACLE)
+	@echo "torch not importable: skipping the optional $(TORCH_EXT)"
+else
 all: $(LIB) $(ORACLE) $(TORCH_EXT)
+endif
 
 $(TORCH_EXT): dirt_amd/csrc/torch_op.cpp include/dirt_mi355x.h
 	g++ $(EXT_CXXFLAGS) -o $@ $< $(EXT_LDFLAGS)

@@ -27,10 +27,11 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
-BWD_ACCUMULATE = 1     # dirt_rasterise_bwd flags
+BWD_ACCUMULATE = 1     # dirt_rasterise_bwd / dirt_rasterise_bwd_recompute flags
+BWD_SCRATCH_CLEAN = 2  # dirt_rasterise_bwd_recompute: the workspace's bin counters are clean
 
 # every symbol include/dirt_mi355x.h declares, with its ctypes signature
 _P = ctypes.c_void_p
@@ -47,6 +48,9 @@ SIGNATURES = {
                                         _P, _P, _P, _P, _P, _P]),
     "dirt_hill_fwd": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _P]),
     "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _U, _P]),
+    "dirt_bwd_recompute_workspace_size": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(_SZ)]),
+    "dirt_rasterise_bwd_recompute": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _U,
+                                          _P]),
     "dirt_scratch_clear": (_I, [_I, _I, _I, _I, _I64, _P, _SZ, _P]),
     "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
     "dirt_profile_enable": (_I, [_I]),
@@ -100,6 +104,13 @@ def workspace_sizes(B, H, W, C, V, F, bin_capacity=0):
     scratch = ctypes.c_size_t(0)
     check(lib.dirt_workspace_sizes(B, H, W, C, V, F, bin_capacity, ctypes.byref(saved), ctypes.byref(scratch)))
     return saved.value, scratch.value
+
+
+@functools.lru_cache(maxsize=256)
+def recompute_workspace_size(B, H, W, C, V, F):
+    n = ctypes.c_size_t(0)
+    check(load().dirt_bwd_recompute_workspace_size(B, H, W, C, V, F, ctypes.byref(n)))
+    return n.value
 
 
 NUM_KERNELS = 3

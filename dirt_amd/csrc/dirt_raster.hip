@@ -241,7 +241,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 7; }
+int dirt_abi_version(void) { return 8; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -266,7 +266,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
                               int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes,
                               void *scratch, size_t scratch_bytes, int64_t bin_capacity, unsigned flags,
                               float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream_,
-                              GbufOut gbo = GbufOut{})
+                              GbufOut gbo = GbufOut{}, bool nopix = false)
 {
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
@@ -280,8 +280,11 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     if (shader_id == DIRT_SHADER_HILL && tcb != 1 && tcb != 3 && tcb != 4)
         return fail(DIRT_EINVAL, "Hill: the terrain lookup must have 1, 3 or 4 channels");
     if (B == 0) return DIRT_OK;
-    const bool need_colors = shader_id == DIRT_SHADER_GOURAUD;
-    if (!background || !pixels || !gbuffer || !saved || !scratch || (F > 0 && (!faces || !vertices)) ||
+    if (nopix && (shader_id != DIRT_SHADER_GOURAUD || want_gb))
+        return fail(DIRT_EINVAL, "Rasterise: the coverage-only pass is Gouraud without G-buffer outputs");
+    // (nopix: the coverage-only pass of dirt_rasterise_bwd_recompute reads no background or colours)
+    const bool need_colors = shader_id == DIRT_SHADER_GOURAUD && !nopix;
+    if ((!nopix && (!background || !pixels)) || !gbuffer || !saved || !scratch || (F > 0 && (!faces || !vertices)) ||
         (V > 0 && (!vertices || (need_colors && !vertex_colors))))
         return fail(DIRT_EINVAL, "Rasterise: null tensor pointer");
     Layout L;
@@ -328,6 +331,18 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
         LAUNCH_PROC(CC, DIRT_SHADER_HILL);                                                                       \
     else if (shader_id >= DIRT_SHADER_OCEANIC)                                                                   \
         LAUNCH_PROC(CC, DIRT_SHADER_OCEANIC);                                                                    \
+    else if (nopix && fused)                                                                                     \
+        raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, false, true, true><<<grid, dim3(256), 0, stream>>>(            \
+            background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
+            L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
+            zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo, faces);   \
+    else if (nopix)                                                                                              \
+        raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, false, false, true><<<grid, dim3(256), 0, stream>>>(           \
+            background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
+            L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
+            zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo);          \
     else if (fused && want_gb)                                                                                   \
         raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, true, true><<<grid, dim3(256), 0, stream>>>(                   \
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
@@ -451,6 +466,67 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
 #undef LAUNCH_GRAD
     HIP_TRY(hipGetLastError());
     return DIRT_OK;
+}
+
+// Workspace of the recompute backward: [saved | scratch | g-buffer], each 256-B aligned
+static void recompute_parts(const Layout &L, int B, int H, int W, size_t &off_scratch, size_t &off_gbuf, size_t &total)
+{
+    off_scratch = (size_t)align_up((int64_t)L.saved_total, 256);
+    off_gbuf = off_scratch + (size_t)align_up((int64_t)L.scratch_total, 256);
+    total = off_gbuf + (size_t)align_up((int64_t)B * H * W * 4, 256);
+}
+
+int dirt_bwd_recompute_workspace_size(int B, int H, int W, int C, int V, int F, size_t *workspace_bytes)
+{
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    size_t os, og, tot;
+    recompute_parts(L, B, H, W, os, og, tot);
+    if (workspace_bytes) *workspace_bytes = tot;
+    return DIRT_OK;
+}
+
+// The registered gradient of the single-output op: upstream DIRT's gradient re-derived its G-buffer from the
+// op's inputs (csrc/rasterise_grad_common.h:5-24: launch_vertex_upload, then launch_grad_assembly on pixels,
+// grad_pixels and vertices).  Here: setup + binning + a coverage-only raster pass (g-buffer and the
+// neighbour-coverage bits, bit-identical to the forward's: same integer rules, same inputs) into the
+// caller's workspace, then the same backward kernel as dirt_rasterise_bwd.
+int dirt_rasterise_bwd_recompute(const float *background, const float *vertices, const float *vertex_colors,
+                                 const int32_t *faces, const float *pixels, const float *grad_pixels, int B, int H,
+                                 int W, int C, int V, int F, float *grad_vertices, float *grad_vertex_colors,
+                                 float *grad_background, void *workspace, size_t workspace_bytes, unsigned flags,
+                                 void *stream_)
+{
+    (void)background;  // part of the op's inputs (the gradient of an uncovered pixel does not depend on it)
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    if (B == 0) return DIRT_OK;
+    if (!pixels || !grad_pixels || !grad_background || !workspace || (F > 0 && (!faces || !vertices)) ||
+        (V > 0 && (!grad_vertices || !grad_vertex_colors)))
+        return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    size_t os, og, tot;
+    recompute_parts(L, B, H, W, os, og, tot);
+    if (workspace_bytes < tot)
+        return fail(DIRT_EINVAL, "RasteriseGrad: workspace smaller than dirt_bwd_recompute_workspace_size()");
+    char *ws = static_cast<char *>(workspace);
+    int32_t *gbuf = reinterpret_cast<int32_t *>(ws + og);
+    const bool acc = (flags & DIRT_BWD_ACCUMULATE) != 0;
+    // the recomputation zero-fills the gradient accumulators in passing (setup filler workgroups), so the
+    // backward below only adds into them
+    rc = rasterise_fwd_impl(nullptr, C, vertices, nullptr, faces, nullptr, B, H, W, C, V, F, DIRT_SHADER_GOURAUD,
+                            nullptr, gbuf, ws, L.saved_total, ws + os, L.scratch_total, 0,
+                            (flags & DIRT_BWD_SCRATCH_CLEAN) ? DIRT_FWD_SCRATCH_CLEAN : 0u,
+                            acc ? nullptr : grad_vertices, acc ? nullptr : grad_vertex_colors, stream_, GbufOut{},
+                            /*nopix=*/true);
+    if (rc) return rc;
+    return dirt_rasterise_bwd(vertices, vertex_colors, faces, pixels, grad_pixels, gbuf, ws, B, H, W, C, V, F,
+                              grad_vertices, grad_vertex_colors, grad_background, DIRT_BWD_ACCUMULATE, stream_);
 }
 
 // Ablation entry point (tools/ablate.py): re-runs raster_kernel (C == 3) on the bins a preceding

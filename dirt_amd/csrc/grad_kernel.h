@@ -649,27 +649,23 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             const float half = axis == 0 ? ns.half_w : ns.half_h;
             const float mid = axis == 0 ? (float)(ilo + 1) : (float)(jlo + 1);
             const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
+            // lambda_k / Wm = a_k / sum_k (a_k w_k) = a_k / (2E_0 + 2E_1 + 2E_2 + st_0 + st_1 + st_2) = a_k / (2D)
+            // (iw_k w_k = 1, the edge functions sum to the constant D and their steps to 0): no division per
+            // pair and nothing to cancel.  A clipped face's sub-triangle maps the same weights of its own
+            // vertices through the clip basis to the parent's: its vertices are convex combinations of the
+            // parent's (w_sub = basis . w), so parent lambda_i / Wm = sum_k a_k basis_ki / (2D) of the
+            // sub-triangle -- the normalised form lambda = a / sum a, Wm = sum lambda w cancelled
+            // on slivers.
+            const float c = omega * s * half * h2d;
             float g[3];
             if (!multi) {
-                // Non-clipped face (identity basis, iw_k w_k = 1): lambda_k / Wm = a_k / sum_k (a_k w_k)
-                // = a_k / (2E_0 + 2E_1 + 2E_2 + st_0 + st_1 + st_2) = a_k / (2D), since the edge
-                // functions sum to the constant D and their steps to 0 -- no division per pair
-                const float c = omega * s * half * h2d;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) g[k] = c * m[k];
             } else {
-                float lm[3];
-                if (!fast_lambda(rec(), multi, m[0], m[1], m[2], lm)) continue;
-                // clip w of the parent vertices, read here (clipped faces only) to keep them out of
-                // the registers of the common path
-                const float w0 = sp >= 0 ? T.q[0][sp] : fdata_frame[f].q[0];
-                const float w1 = sp >= 0 ? T.q[1][sp] : fdata_frame[f].q[1];
-                const float w2 = sp >= 0 ? T.q[2][sp] : fdata_frame[f].q[2];
-                const float Wm = (lm[0] * w0 + lm[1] * w1) + lm[2] * w2;
-                if (Wm == 0.0f) continue;
-                const float tt = omega * s * half * __builtin_amdgcn_rcpf(Wm);
+                const Rec &rr = rec();
 #pragma unroll
-                for (int k = 0; k < 3; ++k) g[k] = tt * lm[k];
+                for (int k = 0; k < 3; ++k)
+                    g[k] = c * ((m[0] * rr.basis[k] + m[1] * rr.basis[3 + k]) + m[2] * rr.basis[6 + k]);
             }
 #pragma unroll
             for (int k = 0; k < 3; ++k) {

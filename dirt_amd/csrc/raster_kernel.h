@@ -397,7 +397,9 @@ struct GbufOut {
 // and FaceData of its frame to `saved` for the backward.  One launch instead of two for small scenes.
 constexpr int kFusedMaxF = 32;
 
-template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false>
+// NOPIX (Gouraud): coverage-only resolve for dirt_rasterise_bwd_recompute -- the g-buffer and the
+// neighbour-coverage bits the backward reads, no pixels (no background or colour loads, no pixel stores).
+template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false, bool NOPIX = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
@@ -414,6 +416,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     static_assert(!(GB && kNoDepth), "hill has no depth buffer");
     static_assert(!FUSED || SH == DIRT_SHADER_GOURAUD, "the fused small-scene forward is Gouraud only");
+    static_assert(!NOPIX || (SH == DIRT_SHADER_GOURAUD && !GB), "the coverage-only resolve is Gouraud only");
     // FUSED: the frame's records and FaceData, set up in LDS by this workgroup
     __shared__ Rec s_recs[FUSED ? (1 + kExtraPerFace) * kFusedMaxF : 1];
     __shared__ FaceData s_fd[FUSED ? kFusedMaxF : 1];
@@ -746,9 +749,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             if (gbo.face) gbo.face[o] = -1;
         }
         if constexpr (SH == DIRT_SHADER_GOURAUD) covbits[o] = 0;
+        if constexpr (!NOPIX) {
 #pragma unroll
-        for (int c2 = 0; c2 < CM; ++c2)
-            if (c2 < C) out[c2] = kNoDepth ? 0.0f : background[o * C + c2];  // (hill: no background copy)
+            for (int c2 = 0; c2 < CM; ++c2)
+                if (c2 < C) out[c2] = kNoDepth ? 0.0f : background[o * C + c2];  // (hill: no background copy)
+        }
         PHASE_TS(4);
         PHASE_TS(5);
         return;
@@ -870,7 +875,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                (float)W, (float)H);
         for (int k = 0; k < C; ++k) out[k] = k == 0 ? col.x : k == 1 ? col.y : k == 2 ? col.z : k == 3 ? 1.0f : 0.0f;
     } else {
-        if (AB & 64) {
+        if constexpr (NOPIX) {
+            // (coverage only: the caller holds the pixels)
+        } else if (AB & 64) {
             for (int k = 0; k < C; ++k) out[k] = lam[k % 3];
         } else {
             const float *cb = colors + (int64_t)b * V * C;

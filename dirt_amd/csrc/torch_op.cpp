@@ -65,29 +65,60 @@ void init(const std::string &path)
 
 // Forward-only scratch (bins, bin counters) per (device, stream, layout), cleared once: every forward
 // leaves it clean for the next one of the same layout (DIRT_FWD_SCRATCH_CLEAN).  LRU of a few layouts.
+// An entry used while its stream is capturing a HIP graph is pinned (the graph's replays write it and nothing
+// else holds a reference): eviction and clear() skip it, clear(force) drops it.  An entry whose forward failed
+// is discarded (its alternating count sets may be dirty).
 struct ScratchCache {
     typedef std::tuple<int, uintptr_t, int64_t, int64_t, int64_t, int64_t, int64_t> Key;
+    struct Entry {
+        Key key;
+        at::Tensor t;
+        bool pinned;
+    };
     std::mutex mu;
-    std::list<std::pair<Key, at::Tensor>> lru;
+    std::list<Entry> lru;
+    static bool capturing(hipStream_t stream)
+    {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        return hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+    }
+    void evict()
+    {
+        size_t n = lru.size();
+        for (auto it = lru.end(); n > 4 && it != lru.begin();) {
+            --it;
+            if (!it->pinned) {
+                it = lru.erase(it);
+                --n;
+            }
+        }
+    }
     at::Tensor get(const Key &k, size_t bytes, const at::Device &dev, hipStream_t stream)
     {
+        const bool cap = capturing(stream);
         std::lock_guard<std::mutex> g(mu);
         for (auto it = lru.begin(); it != lru.end(); ++it)
-            if (it->first == k) {
+            if (it->key == k) {
+                it->pinned = it->pinned || cap;
                 lru.splice(lru.begin(), lru, it);
-                return it->second;
+                return lru.front().t;
             }
         at::Tensor t = at::empty({(int64_t)std::max<size_t>(bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
         check(g_api.scratch_clear((int)std::get<2>(k), (int)std::get<3>(k), (int)std::get<4>(k), (int)std::get<5>(k),
                                   std::get<6>(k), t.data_ptr(), bytes, stream));
-        lru.emplace_front(k, t);
-        while (lru.size() > 4) lru.pop_back();
+        lru.push_front(Entry{k, t, cap});
+        evict();
         return t;
     }
-    void clear()
+    void discard(const Key &k)
     {
         std::lock_guard<std::mutex> g(mu);
-        lru.clear();
+        lru.remove_if([&](const Entry &e) { return e.key == k; });
+    }
+    void clear(bool force)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        lru.remove_if([&](const Entry &e) { return force || !e.pinned; });
     }
     size_t size()
     {
@@ -130,12 +161,20 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
             at::Tensor flag = at::empty({256}, at::TensorOptions().dtype(at::kByte).device(dev));
             check(g_api.check_faces(faces.data_ptr<int32_t>(), (int)B, (int)V, (int)F, flag.data_ptr(), 256, stream));
         }
-        at::Tensor scratch = g_scratch.get(ScratchCache::Key{dev.index(), reinterpret_cast<uintptr_t>(stream), B, H, W,
-                                                             F, bin_capacity},
-                                           scratch_bytes, dev, stream);
+        const ScratchCache::Key skey{dev.index(), reinterpret_cast<uintptr_t>(stream), B, H, W, F, bin_capacity};
+        at::Tensor scratch = g_scratch.get(skey, scratch_bytes, dev, stream);
         float *zgv = need_grad ? gv.data_ptr<float>() : nullptr;
         float *zgc = need_grad ? gc.data_ptr<float>() : nullptr;
         variable_list out{pixels, gbuffer};
+        // a failed forward may leave the cached scratch's count sets dirty: drop it
+        struct DropOnThrow {
+            const ScratchCache::Key &k;
+            bool armed = true;
+            ~DropOnThrow()
+            {
+                if (armed) g_scratch.discard(k);
+            }
+        } drop{skey};
         if (want_gbuf) {
             at::Tensor depth = at::empty({B, H, W}, f32), bary = at::empty({B, H, W, 3}, f32), face = at::empty({B, H, W}, i32);
             check(g_api.fwd_gbuffer(background.data_ptr<float>(), vertices.data_ptr<float>(),
@@ -155,6 +194,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
                             saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, DIRT_FWD_SCRATCH_CLEAN, zgv,
                             zgc, stream));
         }
+        drop.armed = false;
         ctx->save_for_backward({vertices, vertex_colors, faces, pixels, gbuffer, saved});
         ctx->saved_data["dims"] = std::vector<int64_t>{B, H, W, C, V, F, shader_id};
         ctx->saved_data["prezeroed"] = need_grad;
@@ -224,6 +264,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
     m.doc() = "dirt_amd rasterise op: C++ autograd function over the C ABI of libdirt_mi355x.so";
     m.def("init", &init, "dlopen libdirt_mi355x.so and resolve the C ABI");
     m.def("rasterise", &rasterise, "rasterise forward (+ registered backward)");
-    m.def("scratch_cache_clear", []() { g_scratch.clear(); });
+    m.def("scratch_cache_clear", [](bool force) { g_scratch.clear(force); }, py::arg("force") = false);
     m.def("scratch_cache_size", []() { return g_scratch.size(); });
 }

@@ -1,0 +1,114 @@
+"""The reference's op library, single-output: what `tf.load_op_library(_lib_path + '/librasterise.so')`
+returns at dirt/rasterise_ops.py:6-7, restated over libdirt_mi355x.so.
+
+`load_op_library().rasterise(background, vertices, vertex_colors, faces, camera_pos, height, width, channels,
+name=None)` has the signature of REGISTER_OP("Rasterise") (csrc/rasterise_egl.cpp:33-53: inputs background
+[B,H,W,C], vertices [B,V,4], vertex_colors [B,V,C], faces [B,F,3], camera_pos; attrs height, width, channels)
+and, like it, returns ONE tensor, pixels [B,H,W,C] -- so the reference's own wrapper body
+`_rasterise_module.rasterise(...)[0]` (dirt/rasterise_ops.py:50-54) runs unchanged on top of it.
+
+Its gradient is registered the way a TensorFlow maintainer would register it for the single-output op
+(`@tf.RegisterGradient("Rasterise")`): from the op's inputs, its output and
+grad_pixels only, through `dirt_rasterise_bwd_recompute` (include/dirt_mi355x.h), which re-derives the
+g-buffer on the device as upstream DIRT's gradient did (csrc/rasterise_grad_common.h:5-24).  Nothing is kept
+between the forward and the backward except what autograd keeps for any op (inputs and output), and every
+buffer is allocated per call (TF's allocate_temp): no cached state, so the op is safe under graph capture.
+
+The public `dirt_amd.rasterise` keeps the stateful backward (forward state kept for the gradient, no
+recomputation): it is the faster path; this module is the drop-in boundary the north star names.
+"""
+import torch
+
+from . import _lib
+from .rasterise_ops import _as_tensor, _camera, _check_shapes, _device_of, _on_device, _upstream_positional
+
+__all__ = ["load_op_library", "RasteriseOpModule"]
+
+
+class _RasteriseSingleOutput(torch.autograd.Function):
+    """REGISTER_OP("Rasterise") with one output and the recompute-mode registered gradient."""
+
+    @staticmethod
+    def forward(ctx, background, vertices, vertex_colors, faces, camera_pos, H, W, C):
+        B, V, F = vertices.shape[0], vertices.shape[1], faces.shape[1]
+        dev = vertices.device
+        lib = _lib.load()
+        saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, 0)
+        pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+        # temporaries of the forward only (TF: allocate_temp); the gradient recomputes what it needs
+        gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+        saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
+        scratch = torch.empty((max(scratch_bytes, 1),), dtype=torch.uint8, device=dev)
+        with _on_device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            cam = camera_pos.data_ptr() if camera_pos is not None else None
+            _lib.check(lib.dirt_rasterise_fwd(
+                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
+                B, H, W, C, V, F, _lib.SHADER_GOURAUD, pixels.data_ptr(), gbuffer.data_ptr(),
+                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, 0, 0, None, None, stream))
+        # what TF hands a registered gradient: op.inputs and op.outputs
+        ctx.save_for_backward(background, vertices, vertex_colors, faces, pixels)
+        ctx.dims = (B, H, W, C, V, F)
+        return pixels
+
+    @staticmethod
+    def backward(ctx, grad_pixels):
+        background, vertices, vertex_colors, faces, pixels = ctx.saved_tensors
+        return rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, ctx.dims) \
+            + (None,) * 5
+
+
+def rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, dims=None):
+    """The registered gradient of the single-output op: (grad_background, grad_vertices, grad_vertex_colors)
+    from the op's inputs, its output `pixels` and `grad_pixels` (C ABI dirt_rasterise_bwd_recompute)."""
+    if dims is None:
+        B, H, W, C = pixels.shape
+        dims = (B, H, W, C, vertices.shape[1], faces.shape[1])
+    B, H, W, C, V, F = dims
+    dev = vertices.device
+    lib = _lib.load()
+    grad_pixels = grad_pixels.to(dtype=torch.float32).contiguous()
+    nbytes = _lib.recompute_workspace_size(B, H, W, C, V, F)
+    workspace = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
+    grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
+    grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+    with _on_device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.dirt_rasterise_bwd_recompute(
+            background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
+            pixels.data_ptr(), grad_pixels.data_ptr(), B, H, W, C, V, F, grad_vertices.data_ptr(),
+            grad_colors.data_ptr(), grad_background.data_ptr(), workspace.data_ptr(), nbytes, 0, stream))
+    return grad_background, grad_vertices, grad_colors
+
+
+class RasteriseOpModule:
+    """The object `tf.load_op_library` returns for librasterise.so, reduced to the `Rasterise` op the north
+    star replaces (the procedural ops are `dirt_amd.rasterise(..., shader=...)` and `dirt_amd.hill`)."""
+
+    def rasterise(self, background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
+                  channels=None, name=None):
+        """REGISTER_OP("Rasterise") (csrc/rasterise_egl.cpp:33-53): pixels [B,H,W,C], one output.  Upstream's
+        attribute-only call (`rasterise(bg, v, c, f, height, width, channels)`, dirt/rasterise_ops.py:84-88)
+        binds height to the camera_pos slot and is accepted the same way as by dirt_amd.rasterise_batch."""
+        camera_pos, height, width, channels, name = _upstream_positional(camera_pos, height, width, channels, name)
+        del name
+        dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
+        background = _as_tensor(background, torch.float32, dev).contiguous()
+        vertices = _as_tensor(vertices, torch.float32, dev).contiguous()
+        vertex_colors = _as_tensor(vertex_colors, torch.float32, dev).contiguous()
+        faces = _as_tensor(faces, torch.int32, dev).contiguous()
+        # (the attrs are required by the op: the reference's wrappers infer them from the static shape)
+        H, W, C = int(height), int(width), int(channels)
+        _check_shapes(background, vertices, vertex_colors, faces, H, W, C)
+        cam = _camera(camera_pos, _lib.SHADER_GOURAUD, dev)
+        return _RasteriseSingleOutput.apply(background, vertices, vertex_colors, faces, cam, H, W, C)
+
+
+def load_op_library(path=None):
+    """`tf.load_op_library(path)` for libdirt_mi355x.so (dirt/rasterise_ops.py:7).  `path` is accepted for
+    signature parity; the library is the one dirt_amd._lib loads (DIRT_MI355X_LIB honoured)."""
+    del path
+    _lib.load()
+    return RasteriseOpModule()
+

@@ -68,20 +68,32 @@ class _Workspace:
     A scratch zero-filled once stays clean across forwards of the same layout (the bin counters alternate
     between two sets, include/dirt_mi355x.h DIRT_FWD_SCRATCH_CLEAN), so a cached one saves every call the
     counter memset (128 MiB for B = 64 at 8192^2 with one 256-B line per counter) and the allocation.
-    Keyed by the stream too: two streams never share a scratch.  A few layouts are kept (LRU)."""
+    Keyed by the stream too: two streams never share a scratch.  A few layouts are kept (LRU).
+
+    Graph capture: a HIP graph captured through the op replays writes into this scratch, and neither the
+    autograd context nor the graph holds a reference to it, so an entry used while its stream was capturing is
+    pinned: LRU eviction and clear() skip it (clear(force=True) drops it too, for callers that have destroyed
+    their graphs).  An entry whose forward failed after its first launch is dropped (`discard`): its
+    alternating bin-count sets may no longer be clean."""
 
     def __init__(self, keep=4):
         self.keep = keep
         self._lock = threading.Lock()
         self._d = collections.OrderedDict()
+        self._pinned = set()
 
     def scratch(self, dev, stream, layout, nbytes):
         key = (dev, stream, layout)
+        capturing = torch.cuda.is_current_stream_capturing()
         with self._lock:
             t = self._d.get(key)
             if t is not None:
                 self._d.move_to_end(key)
+                if capturing:
+                    self._pinned.add(key)
                 return t
+        # (a buffer created during capture comes from the graph's private pool and is cleared once, inside the
+        # graph; each replay's forward leaves it clean for the next, as any forward does)
         # only the bin counters need zeroing (dirt_scratch_clear: a memset of the counter lines); the slabs
         # are written before they are read
         t = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
@@ -89,13 +101,37 @@ class _Workspace:
         _lib.check(_lib.load().dirt_scratch_clear(B, H, W, F, cap, t.data_ptr(), nbytes, stream))
         with self._lock:
             self._d[key] = t
-            while len(self._d) > self.keep:
-                self._d.popitem(last=False)
+            if capturing:
+                self._pinned.add(key)
+            self._evict()
         return t
 
-    def clear(self):
+    def _evict(self):
+        for k in list(self._d):
+            if len(self._d) <= self.keep:
+                break
+            if k not in self._pinned:
+                del self._d[k]
+
+    def discard(self, dev, stream, layout):
         with self._lock:
-            self._d.clear()
+            key = (dev, stream, layout)
+            self._d.pop(key, None)
+            self._pinned.discard(key)
+
+    def clear(self, force=False):
+        with self._lock:
+            if force:
+                self._d.clear()
+                self._pinned.clear()
+            else:
+                for k in list(self._d):
+                    if k not in self._pinned:
+                        del self._d[k]
+
+    def __len__(self):
+        with self._lock:
+            return len(self._d)
 
 
 _workspace = _Workspace()
@@ -131,36 +167,49 @@ class _RasteriseFunction(torch.autograd.Function):
         need_grad = shader_id == _lib.SHADER_GOURAUD and any(ctx.needs_input_grad[:3]) and V > 0
         gv = torch.empty((B, V, 4), dtype=torch.float32, device=dev) if need_grad else None
         gc = torch.empty((B, V, C), dtype=torch.float32, device=dev) if need_grad else None
-        extra = ()
         with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             if check_faces:
                 _check_faces_now(faces, B, V, F, stream)
-            scratch = _workspace.scratch(dev, stream, (B, H, W, F, bin_capacity), scratch_bytes)
+            layout = (B, H, W, F, bin_capacity)
+            scratch = _workspace.scratch(dev, stream, layout, scratch_bytes)
             cam = camera_pos.data_ptr() if camera_pos is not None else None
             zg = (gv.data_ptr(), gc.data_ptr()) if need_grad else (None, None)
-            if want_gbuf:
-                depth = torch.empty((B, H, W), dtype=torch.float32, device=dev)
-                bary = torch.empty((B, H, W, 3), dtype=torch.float32, device=dev)
-                face_ids = torch.empty((B, H, W), dtype=torch.int32, device=dev)
-                _lib.check(lib.dirt_rasterise_fwd_gbuffer(
-                    background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
-                    B, H, W, C, V, F, pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(), saved_bytes,
-                    scratch.data_ptr(), scratch_bytes, bin_capacity, _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1],
-                    depth.data_ptr(), bary.data_ptr(), face_ids.data_ptr(), stream))
-                extra = (depth, bary, face_ids)
-            else:
-                _lib.check(lib.dirt_rasterise_fwd(
-                    background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
-                    B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
-                    saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
-                    _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1], stream))
+            try:
+                extra = _RasteriseFunction._launch(lib, want_gbuf, background, vertices, vertex_colors, faces, cam,
+                                                   B, H, W, C, V, F, shader_id, pixels, gbuffer, saved, saved_bytes,
+                                                   scratch, scratch_bytes, bin_capacity, zg, stream)
+            except Exception:
+                _workspace.discard(dev, stream, layout)  # its count sets may be dirty now
+                raise
         ctx.save_for_backward(vertices, vertex_colors, faces, pixels, gbuffer, saved)
         ctx.dims = (B, H, W, C, V, F)
         ctx.shader_id = shader_id
         ctx.prezeroed = (gv, gc) if need_grad else None
         ctx.mark_non_differentiable(gbuffer, *extra)
         return (pixels, gbuffer) + extra
+
+    @staticmethod
+    def _launch(lib, want_gbuf, background, vertices, vertex_colors, faces, cam, B, H, W, C, V, F, shader_id, pixels,
+                gbuffer, saved, saved_bytes, scratch, scratch_bytes, bin_capacity, zg, stream):
+        """The forward's C-ABI call; returns the extra G-buffer outputs (empty unless want_gbuf)."""
+        if not want_gbuf:
+            _lib.check(lib.dirt_rasterise_fwd(
+                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
+                B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
+                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
+                _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1], stream))
+            return ()
+        dev = vertices.device
+        depth = torch.empty((B, H, W), dtype=torch.float32, device=dev)
+        bary = torch.empty((B, H, W, 3), dtype=torch.float32, device=dev)
+        face_ids = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+        _lib.check(lib.dirt_rasterise_fwd_gbuffer(
+            background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
+            B, H, W, C, V, F, pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(), saved_bytes,
+            scratch.data_ptr(), scratch_bytes, bin_capacity, _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1],
+            depth.data_ptr(), bary.data_ptr(), face_ids.data_ptr(), stream))
+        return (depth, bary, face_ids)
 
     @staticmethod
     def backward(ctx, grad_pixels, _grad_gbuffer, *_grad_extra):
@@ -274,17 +323,18 @@ def _torch_ext():
     return _EXT or None
 
 
-def workspace_cache_clear():
-    """Drop the cached per-layout scratch buffers (both implementations)."""
-    _workspace.clear()
+def workspace_cache_clear(force=False):
+    """Drop the cached per-layout scratch buffers (both implementations).  Buffers a captured HIP graph
+    writes are kept unless `force` (then no graph captured through the op may be replayed again)."""
+    _workspace.clear(force)
     ext = _torch_ext()
     if ext is not None:
-        ext.scratch_cache_clear()
+        ext.scratch_cache_clear(bool(force))
 
 
 def workspace_cache_size():
     ext = _torch_ext()
-    return len(_workspace._d) + (ext.scratch_cache_size() if ext is not None else 0)
+    return len(_workspace) + (ext.scratch_cache_size() if ext is not None else 0)
 
 
 # DIRT_CHECK_FACES=1: every call range-checks its face indices (one kernel + a host sync; off by default)

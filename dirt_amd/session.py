@@ -11,6 +11,12 @@ forward leaves it clean (DIRT_FWD_SCRATCH_CLEAN skips the forward's clearing mem
 zero-fills the gradient accumulators in passing (filler workgroups of its setup launch), so the backward adds into them
 (DIRT_BWD_ACCUMULATE) without a clearing kernel of its own.  Hence: the gradients returned by
 `backward` stay valid until the next `forward`, and each forward is followed by at most one backward.
+
+Streams: the session's buffers are ordered by the stream each call runs on.  A call on a different stream
+than the previous one first makes its stream wait for the previous one (an event, no host sync), so a
+session may move between streams -- e.g. a warm-up on the default stream, then a HIP-graph capture on a
+side stream -- without racing its own buffers.  (Inside a capture no cross-stream wait is inserted: the
+capturing code orders the capture stream itself, as bench.py does with `stream.wait_stream`.)
 """
 import torch
 
@@ -38,10 +44,21 @@ class RasteriseSession:
         self.grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         self._lib = _lib.load()
         self._inputs = None
+        self._last_stream = None
         # clean once (the bin counters; the slabs are written before they are read); every forward leaves
         # it clean
         _lib.check(self._lib.dirt_scratch_clear(B, H, W, F, self.bin_capacity, self.scratch.data_ptr(),
                                                 self.scratch_bytes, torch.cuda.current_stream(dev).cuda_stream))
+        self._last_stream = torch.cuda.current_stream(dev)
+
+    def _stream(self):
+        """The current stream's handle, ordered after the stream of the session's previous call."""
+        cur = torch.cuda.current_stream(self.device)
+        last = self._last_stream
+        if last is not None and last != cur and not torch.cuda.is_current_stream_capturing():
+            cur.wait_stream(last)
+        self._last_stream = cur
+        return cur.cuda_stream
 
     def _check(self, t, shape, dtype):
         if t.device != self.device or t.dtype != dtype or tuple(t.shape) != shape or not t.is_contiguous():
@@ -74,7 +91,7 @@ class RasteriseSession:
         self._check(faces, (B, F, 3), torch.int32)
         cam = self._check_camera(camera_pos)
         self._inputs = (background, vertices, vertex_colors, faces)
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        stream = self._stream()
         _lib.check(self._lib.dirt_rasterise_fwd(
             background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
             B, H, W, C, V, F, self.shader_id, self.pixels.data_ptr(), self.gbuffer.data_ptr(),
@@ -91,7 +108,7 @@ class RasteriseSession:
         B, H, W, C, V, F = self.dims
         self._check(grad_pixels, (B, H, W, C), torch.float32)
         _, vertices, vertex_colors, faces = self._inputs
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        stream = self._stream()
         _lib.check(self._lib.dirt_rasterise_bwd(
             vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), self.pixels.data_ptr(),
             grad_pixels.data_ptr(), self.gbuffer.data_ptr(), self.saved.data_ptr(), B, H, W, C, V, F,

@@ -11,6 +11,9 @@
  *                                 never defined in the fork) -- the gradient DIRT registers upstream
  *                                 for "Rasterise"; the fork's REGISTER_OP("RasteriseGrad")
  *                                 (csrc/rasterise_grad_egl.cpp:33-53) is a forward render
+ *   dirt_rasterise_bwd_recompute  the same gradient from the op's inputs + output + grad_pixels only, for
+ *                                 a single-output `Rasterise` with tf.RegisterGradient (upstream DIRT's
+ *                                 shape: rasterise_grad_common.h:5-24 re-derives its G-buffer)
  *   dirt_hill_fwd       replaces  REGISTER_OP("Hill") + HillOpGpu     csrc/hill.cpp:33-53, 282-498
  *                                 (the other procedural ops are shader ids of dirt_rasterise_fwd:
  *                                 RasteriseGrad, OceanicStillCloud, OceanicNoCloud, OceanicOptFlow,
@@ -68,7 +71,8 @@ extern "C" {
 
 /* ABI version, bumped on any signature or workspace-layout change (4: + dirt_hill_fwd, shader ids 6 and 7;
  * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
- * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer) */
+ * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer; 8: + dirt_rasterise_bwd_recompute,
+ * dirt_bwd_recompute_workspace_size) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -141,6 +145,29 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
 #define DIRT_BWD_ACCUMULATE 1u /* add into grad_vertices / grad_vertex_colors instead of overwriting them
                                   (e.g. zeroed by the caller on a side stream, off the critical path);
                                   grad_background is always overwritten */
+/* Backward of the single-output op: the registered gradient of `Rasterise` computed from the op's own inputs,
+ * its output and grad_pixels only -- nothing kept from the forward, so the TensorFlow op stays
+ * single-output (csrc/rasterise_egl.cpp:33-53; dirt/rasterise_ops.py:50-54 indexes `[0]`).  Replaces upstream
+ * DIRT's gradient path, which re-derived its G-buffer from the op's inputs: launch_vertex_upload +
+ * launch_grad_assembly(grad_vertices, grad_vertex_colors, grad_background, ..., pixels, grad_pixels,
+ * vertices, ...) (csrc/rasterise_grad_common.h:5-24, declared only in the fork).  Recomputes setup, binning
+ * and a coverage-only raster pass (g-buffer + neighbour-coverage bits, bit-identical to the forward's) into
+ * `workspace`, then runs the backward kernel of dirt_rasterise_bwd: the same gradients (up to float-atomic
+ * summation order), at the cost of the forward's setup and a raster pass without pixel traffic.
+ * `pixels` must be the op's output for these inputs.  background / vertex_colors are part of the gradient's
+ * inputs and are not read.  Outputs as dirt_rasterise_bwd (fully overwritten unless DIRT_BWD_ACCUMULATE).
+ * workspace: caller-owned device memory of dirt_bwd_recompute_workspace_size() bytes; no state survives the
+ * call unless DIRT_BWD_SCRATCH_CLEAN is used. */
+int dirt_bwd_recompute_workspace_size(int B, int H, int W, int C, int V, int F, size_t *workspace_bytes);
+int dirt_rasterise_bwd_recompute(const float *background, const float *vertices, const float *vertex_colors,
+                                 const int32_t *faces, const float *pixels, const float *grad_pixels,
+                                 int B, int H, int W, int C, int V, int F,
+                                 float *grad_vertices, float *grad_vertex_colors, float *grad_background,
+                                 void *workspace, size_t workspace_bytes, unsigned flags, void *stream);
+/* flags of dirt_rasterise_bwd_recompute: DIRT_BWD_ACCUMULATE, and */
+#define DIRT_BWD_SCRATCH_CLEAN 2u /* the workspace was zero-filled once and since used only by recompute
+                                     backwards of the same B, H, W, F: skip the bin-counter memset */
+
 /* Zero the bin counters of `scratch` for the next forward with the same B, H, W, F, bin_capacity
  * (an async memset of a few KB; lets a caller clear them on another stream, see DIRT_FWD_SCRATCH_CLEAN). */
 int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *scratch, size_t scratch_bytes,

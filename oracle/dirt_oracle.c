@@ -1315,15 +1315,19 @@ static int covers_face(const orc_rec *recs, const int32_t *nsub, int F, int f, i
 }
 
 /* owner h (record r), pair midpoint between samples (i,j) and (i2,j2), axis 0=x 1=y.
- * `identity`: the record belongs to a face that did not take the clipping path (identity basis, its 1/w the
- * face's own): then lambda_k / Wm = a_k / sum_k (a_k w_k) = a_k / sum_k E_k with a_k = E_k / w_k, and the edge
- * functions at the pair midpoint sum to 2D exactly (E_0 + E_1 + E_2 = D at every sample), so the weight needs
- * no normalisation.  Normalising first (lambda = a / sum a, Wm = sum lambda w) cancels catastrophically on
- * slivers, where the E_k are ~10^3 x D: the fuzz scene of seed 37851 (a 1811-unit sliver) lost 4e-4 relative
- * that way against a float64 evaluation, which the HIP backward (the same exact-2D form) matched to 1e-6. */
+ * dL/dx_k += omega s (W/2) lambda_k / Wm with lambda the perspective-correct parent barycentrics
+ * at the pair midpoint and Wm = sum_k lambda_k w_k (the clip w there).  Evaluated without normalising:
+ * a_k = E_k(mid) / w_k of the record's own vertices, and the edge functions at the midpoint sum to 2D exactly
+ * (E_0 + E_1 + E_2 = D at every sample, an int64 identity), so lambda_k / Wm = a_k / (2D) for a face that did not
+ * take the clipping path; a clipped face's sub-triangle has vertices that are convex combinations of the
+ * parent's (basis rows; w_sub = basis . w_parent), so the parent's lambda_i / Wm = sum_k a_k basis_ki / (2D).
+ * The normalised form (lambda = a / sum a, Wm = sum lambda w) cancels catastrophically on slivers, whose E_k
+ * are ~10^3 x D: the fuzz scene of seed 37851 (a 1811-unit sliver) lost 4e-4 relative that way against a
+ * float64 evaluation (tests/backward_f64.py pins both kinds of face at 1e-6 of the gradient scale). */
 static void add_pair_owner(const orc_rec *r, const float *vb, const int32_t *fb, int W, int H,
                            int i, int j, int i2, int j2, int axis, float s, float omega, int identity, double *gv)
 {
+    (void)vb;
     int64_t E1[3], E2[3], E[3];
     edge_values(r, i, j, E1);
     edge_values(r, i2, j2, E2);
@@ -1332,21 +1336,13 @@ static void add_pair_owner(const orc_rec *r, const float *vb, const int32_t *fb,
     float half = axis == 0 ? 0.5f * (float)W : 0.5f * (float)H;
     float mid = axis == 0 ? (float)(i + 1) : (float)(j + 1);
     float ndc = mid / half - 1.0f;
-    float g3[3];
-    if (identity) {
-        const int64_t twoD = E[0] + E[1] + E[2];
-        if (twoD == 0) return;
-        const float t = ((omega * s) * half) / (float)twoD;
-        for (int k = 0; k < 3; ++k) g3[k] = t * ((float)E[k] * r->iw[k]);
-    } else {
-        float lam[3];
-        if (!parent_lambda(r, E, lam)) return;
-        float w0 = vb[(int64_t)f3[0] * 4 + 3], w1 = vb[(int64_t)f3[1] * 4 + 3], w2 = vb[(int64_t)f3[2] * 4 + 3];
-        float Wm = (lam[0] * w0 + lam[1] * w1) + lam[2] * w2;
-        if (Wm == 0.0f) return;
-        float t = ((omega * s) * half) / Wm;
-        for (int k = 0; k < 3; ++k) g3[k] = t * lam[k];
-    }
+    const int64_t twoD = E[0] + E[1] + E[2];
+    if (twoD == 0) return;
+    const float t = ((omega * s) * half) / (float)twoD;
+    float a[3], g3[3];
+    for (int k = 0; k < 3; ++k) a[k] = (float)E[k] * r->iw[k];
+    for (int k = 0; k < 3; ++k)
+        g3[k] = identity ? t * a[k] : t * ((a[0] * r->basis[k] + a[1] * r->basis[3 + k]) + a[2] * r->basis[6 + k]);
     for (int k = 0; k < 3; ++k) {
         float g = g3[k];
         double *d = gv + (int64_t)f3[k] * 4;

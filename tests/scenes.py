@@ -294,3 +294,62 @@ def adversarial_scene(seed, W=64, H=48, C=3, F=300):
     cols = rng.uniform(0, 1, size=(3 * nf, C)).astype(np.float32)
     bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
     return bg, v, cols, faces
+
+
+def fuzz_case(seed):
+    """The scene of tests/test_gpu_parity.py::test_fuzz_adversarial_scenes for `seed` (a batch of two frames of
+    150 faces when seed % 4 == 3, padded to a common F and V, else one frame)."""
+    W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
+    C = 3 if seed < 36 else (3, 7, 1, 5)[seed % 4]
+    if seed % 4 != 3:
+        return tuple(a[None] for a in adversarial_scene(seed, W=W, H=H, C=C))
+    frames = [adversarial_scene(seed * 10 + k, W=W, H=H, C=C, F=150) for k in range(2)]
+    F = max(fr[3].shape[0] for fr in frames)
+    frames = [(bg, v, c, np.concatenate([f, np.zeros((F - f.shape[0], 3), np.int32)])) for bg, v, c, f in frames]
+    V = max(fr[1].shape[0] for fr in frames)
+    frames = [(bg, np.concatenate([v, np.tile(v[:1], (V - v.shape[0], 1))]),
+               np.concatenate([c, np.tile(c[:1], (V - c.shape[0], 1))]), f) for bg, v, c, f in frames]
+    return tuple(np.stack([fr[k] for fr in frames]) for k in range(4))
+
+
+def clipped_sliver_scene(seed, W=48, H=40, C=3, n=10):
+    """Faces that take the R5 clipping path and are slivers once clipped -- the case whose normalised pair
+    weight (lambda = a / sum a, Wm = sum lambda w) cancels:
+      * guard-band slivers: two vertices ~1000x the frame away along a line through it (clipped by the guard
+        planes), the third 0.02..3 px off that line;
+      * near-plane slivers: one vertex behind the eye (w < 0), the other two a fraction of a pixel apart;
+      * a few ordinary faces in front of and behind them (occlusion boundaries), random depths."""
+    rng = np.random.default_rng(seed)
+    tris = []
+    px2ndc = np.array([2.0 / W, 2.0 / H])
+    for _ in range(n):
+        kind = rng.integers(0, 3)
+        z = rng.uniform(-0.8, 0.8)
+        if kind == 0:
+            p = rng.uniform(-0.8, 0.8, 2)
+            a = rng.uniform(0, np.pi)
+            d = np.array([np.cos(a), np.sin(a)])
+            L = rng.uniform(800.0, 3000.0)
+            off = np.array([-d[1], d[0]]) * px2ndc * rng.uniform(0.02, 3.0)
+            q = p + rng.uniform(-0.5, 0.5) * d + off
+            t = [[*(p - L * d), z, 1.0], [*(p + L * d), z, 1.0], [*q, z, 1.0]]
+        elif kind == 1:
+            p = rng.uniform(-0.8, 0.8, 2)
+            e = rng.uniform(-1, 1, 2)
+            e = e / np.linalg.norm(e) * px2ndc * rng.uniform(0.05, 0.8)
+            wb = rng.uniform(-1.5, -0.05)
+            back = rng.uniform(-1, 1, 2)
+            w1, w2 = rng.uniform(0.5, 2.0, 2)
+            t = [[back[0] * abs(wb), back[1] * abs(wb), z * abs(wb), wb],
+                 [p[0] * w1, p[1] * w1, z * w1, w1], [(p[0] + e[0]) * w2, (p[1] + e[1]) * w2, z * w2, w2]]
+        else:
+            c = rng.uniform(-0.9, 0.9, 2)
+            o = rng.uniform(-0.6, 0.6, size=(3, 2))
+            t = [[*(c + oo), z, 1.0] for oo in o]
+        tris.append(t)
+    v = np.array(tris, np.float64).reshape(-1, 4).astype(np.float32)
+    nf = len(tris)
+    faces = np.arange(3 * nf, dtype=np.int32).reshape(nf, 3)
+    cols = rng.uniform(0, 1, size=(3 * nf, C)).astype(np.float32)
+    bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
+    return bg, v, cols, faces

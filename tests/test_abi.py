@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_workspace_sizes():
     lib = _lib.load()
-    assert lib.dirt_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.dirt_abi_version() == _lib.ABI_VERSION == 8
     saved, scratch = _lib.workspace_sizes(1, 1024, 1024, 3, 150000, 50000)
     assert saved >= 50000 * 6 * 128 + 50000 * 32  # 128-B records (6 slots/face) + 32-B face data
     assert scratch > 0
@@ -91,4 +91,22 @@ def test_cpp_autograd_extension_builds_and_binds():
     from dirt_amd import rasterise_ops
     ext = rasterise_ops._torch_ext()
     assert ext is not None
+    rasterise_ops.workspace_cache_clear()
     assert ext.scratch_cache_size() == 0
+
+
+def test_recompute_backward_validates_without_a_gpu():
+    """dirt_rasterise_bwd_recompute (the single-output op's gradient, csrc/rasterise_grad_common.h:5-24 shape):
+    its workspace size is the forward's saved + scratch + a g-buffer, and bad arguments are refused before any
+    HIP call."""
+    lib = _lib.load()
+    n = _lib.recompute_workspace_size(1, 1024, 1024, 3, 150000, 50000)
+    saved, scratch = _lib.workspace_sizes(1, 1024, 1024, 3, 150000, 50000)
+    assert n >= saved + scratch + 4 * 1024 * 1024
+    with pytest.raises(ValueError, match="channels"):
+        _lib.recompute_workspace_size(1, 16, 16, 9, 3, 1)
+    args = [None] * 6 + [1, 16, 16, 3, 3, 1] + [None] * 4 + [0, 0, None]
+    assert lib.dirt_rasterise_bwd_recompute(*args) == _lib.DIRT_EINVAL
+    assert "null" in lib.dirt_last_error().decode()
+    args = [None] * 6 + [0, 16, 16, 3, 3, 1] + [None] * 4 + [0, 0, None]
+    assert lib.dirt_rasterise_bwd_recompute(*args) == _lib.DIRT_OK  # B == 0: nothing to do

@@ -212,6 +212,91 @@ def test_hip_graph_capture_of_autograd_path():
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
 
 
+@pytest.mark.parametrize("impl", ["ext", "py"])
+def test_captured_graph_survives_cache_eviction_and_clear(impl):
+    """a HIP graph captured through the public op replays writes into the op's cached scratch.
+    After capture, clearing the cache and churning it with other layouts must not free that scratch: the
+    entry is pinned while its stream captured.  Capture, clear + evict + allocate over the freed pool,
+    replay, compare with the eager result."""
+    from dirt_amd import rasterise_ops
+    ext = rasterise_ops._torch_ext()
+    if impl == "ext":
+        assert ext is not None
+
+    def op(t0, t1, t2, ft, H, W, C):
+        args = (t0, t1, t2, ft, None, H, W, C, 0, 0, False, False)
+        return ext.rasterise(*args) if impl == "ext" else rasterise_ops._RasteriseFunction.apply(*args)
+
+    rasterise_ops.workspace_cache_clear(force=True)
+    bg, v, c, f = (a[None] for a in scenes.random_triangles(F=2500, W=160, H=128, radius_px=10.0, seed=86))
+    B, H, W, C = bg.shape
+    t = [_gpu(a).requires_grad_(True) for a in (bg, v, c)]
+    ft = _gpu(f)
+    g = torch.randn(bg.shape, device="cuda")
+    outs = {}
+
+    def step():
+        px, _ = op(t[0], t[1], t[2], ft, H, W, C)
+        outs["px"] = px
+        outs["grads"] = torch.autograd.grad(px, t, g)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.synchronize()
+    ref_px = outs["px"].detach().clone()
+    ref_g = [x.clone() for x in outs["grads"]]
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        step()
+    torch.cuda.synchronize()
+    # churn the cache: clear (non-forced) and six other layouts on the default stream, then fill fresh
+    # allocations with garbage so that a freed scratch would be overwritten
+    rasterise_ops.workspace_cache_clear()
+    for k in range(6):
+        bg2, v2, c2, f2 = (a[None] for a in scenes.random_triangles(F=300 + 50 * k, W=48 + 8 * k, H=40, seed=87 + k))
+        op(_gpu(bg2), _gpu(v2), _gpu(c2), _gpu(f2), 40, 48 + 8 * k, 3)
+    junk = [torch.full((1 << 22,), -7, dtype=torch.int32, device="cuda") for _ in range(16)]
+    torch.cuda.synchronize()
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(outs["px"], ref_px)
+    assert torch.equal(outs["grads"][0], ref_g[0])
+    for a, b in zip(outs["grads"][1:], ref_g[1:]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
+    del junk, graph
+    rasterise_ops.workspace_cache_clear(force=True)
+    assert rasterise_ops.workspace_cache_size() == 0
+
+
+def test_session_moves_between_streams():
+    """RasteriseSession orders each call after the stream of its previous call: forward on one side stream,
+    backward on another, no explicit synchronisation -- the gradients equal the single-stream ones."""
+    from dirt_amd.session import RasteriseSession
+    bg, v, c, f = (a[None] for a in scenes.random_triangles(F=20000, W=512, H=512, radius_px=12.0, seed=88))
+    ts = [_gpu(a) for a in (bg, v, c, f)]
+    g = torch.randn(bg.shape, device="cuda")
+    sess = RasteriseSession(*bg.shape, v.shape[1], f.shape[1], device="cuda")
+    sess.forward(*ts)
+    ref = [x.clone() for x in sess.backward(g)]
+    ref_px = sess.pixels.clone()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(s1):
+            sess.forward(*ts)
+        with torch.cuda.stream(s2):
+            out = sess.backward(g)
+            res = [x.clone() for x in out] + [sess.pixels.clone()]
+        torch.cuda.current_stream().wait_stream(s2)
+        torch.cuda.synchronize()
+        assert torch.equal(res[3], ref_px)
+        assert torch.equal(res[0], ref[0])
+        for a, b in zip(res[1:3], ref[1:]):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
+
+
 @pytest.mark.parametrize("want_gbuf", [False, True])
 def test_cpp_autograd_op_matches_python_function(want_gbuf):
     """The public op runs the C++ autograd function (_dirt_torch, dirt_amd/csrc/torch_op.cpp) when built;
