@@ -28,7 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
 # measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc passes of this bench at c3;
 # produced by tools/gpu_traffic.sh + tools/pmc_traffic.py, committed with the round's profiles)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04", "traffic.json")
+if not os.path.exists(TRAFFIC_JSON):
+    TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "traffic.json")
 
 CONFIGS = {
     # name: (B per rank, H, W, C, F, radius_px)
@@ -81,6 +83,24 @@ def host_cpu_info():
     return {"cpu_model": model, "nproc_online": os.cpu_count(), "affinity_cpus": affinity}
 
 
+def cpu_share():
+    """Evidence for the CPU share the baseline runs on: the cgroup CPU quota (cgroup v2 cpu.max, v1
+    cfs_quota / cfs_period), the cpuset, OMP_NUM_THREADS as the box sets it, and the CPUs online."""
+    out = {"OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "nproc_online": os.cpu_count()}
+    for key, path in (("cgroup_cpu_max", "/sys/fs/cgroup/cpu.max"),
+                      ("cgroup_cpuset_effective", "/sys/fs/cgroup/cpuset.cpus.effective"),
+                      ("cgroup_v1_cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"),
+                      ("cgroup_v1_cfs_period_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            out[key] = open(path).read().strip()
+        except OSError:
+            pass
+    q = out.get("cgroup_cpu_max", "").split()
+    if len(q) == 2 and q[0] != "max":
+        out["cgroup_cpu_quota_cpus"] = round(int(q[0]) / int(q[1]), 2)
+    return out
+
+
 def cpu_threads():
     """Every host core this job may use: the CPU share the pool grants one GPU's job (OMP_NUM_THREADS, which
     the GPU box sets; the box's rules size worker pools to that share), else the process's affinity mask."""
@@ -111,6 +131,7 @@ def cpu_baseline(host, grad_host, budget_s=10.0, max_reps=20):
                      "OpenMP, %d threads" % (B, H, W, C, f.shape[1], len(times), nthreads),
            "ms_per_frame": t * 1e3 / B}
     out.update(host_cpu_info())
+    out["cpu_share"] = cpu_share()
     return out, (px, gb) + tuple(grads)
 
 
@@ -184,6 +205,7 @@ def main():
                          "working set exceeds the 256 MiB Infinity Cache; 0 = skip")
     ap.add_argument("--no-api-leg", action="store_true", help="skip the public rasterise_batch + autograd leg")
     ap.add_argument("--no-gather-leg", action="store_true", help="N > 1: skip the RCCL all-gather leg")
+    ap.add_argument("--no-recompute-leg", action="store_true", help="skip the recompute-backward leg")
     ap.add_argument("--min-warm-ms", type=float, default=200.0,
                     help="after the warmup steps, keep running the step untimed for this long (GPU clock ramp); "
                          "0 = off")
@@ -372,6 +394,62 @@ def main():
     if not args.no_api_leg:
         leg("api_autograd", api_leg)
 
+    def recompute_leg():
+        """The single-output op's gradient (dirt_rasterise_bwd_recompute): forward + recompute backward per
+        step, graph-captured like the headline step, against the stateful session step."""
+        lib = _lib.load()
+        n_ws = _lib.recompute_workspace_size(B, H, W, C, V, F)
+        ws = torch.zeros((n_ws,), dtype=torch.uint8, device=device)
+        gv = torch.empty((B, V, 4), device=device)
+        gc = torch.empty((B, V, C), device=device)
+        gbg = torch.empty((B, H, W, C), device=device)
+
+        def rc_bwd():
+            stream = torch.cuda.current_stream(device).cuda_stream
+            _lib.check(lib.dirt_rasterise_bwd_recompute(
+                bg.data_ptr(), v.data_ptr(), c.data_ptr(), f.data_ptr(), sess.pixels.data_ptr(), grad.data_ptr(),
+                B, H, W, C, V, F, gv.data_ptr(), gc.data_ptr(), gbg.data_ptr(), ws.data_ptr(), n_ws,
+                _lib.BWD_SCRATCH_CLEAN, stream))
+
+        def rc_step():
+            sess.forward(bg, v, c, f)
+            rc_bwd()
+
+        for _ in range(5):
+            rc_step()
+        n_rc = max(20, args.steps)
+        g_rc = graph_of(rc_step, min(n_rc, 200), cap_stream) if not args.no_graph else None
+        reps = max(1, n_rc // min(n_rc, 200)) if g_rc else n_rc
+        t_rc = timed(g_rc.replay if g_rc else rc_step, reps, barrier, world, device, shared)
+        steps_rc = reps * (min(n_rc, 200) if g_rc else 1)
+        kr = kernel_times(rc_bwd, args.profile_steps)
+        g_b = graph_of(rc_bwd, 50, cap_stream) if not args.no_graph else None
+        bwd_graph_us = None
+        if g_b is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g_b.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            bwd_graph_us = round(e0.elapsed_time(e1) * 1e3 / 50, 2)
+        legs["recompute_bwd"] = {
+            "what": "forward + dirt_rasterise_bwd_recompute per step (the single-output op's registered gradient: "
+                    "setup + bins + coverage-only raster + backward kernel from the op's inputs, output and "
+                    "grad_pixels), workspace zero-filled once",
+            "mpix_s": round(world * B * H * W * steps_rc / t_rc / 1e6, 1),
+            "ms_per_step": round(t_rc * 1e3 / steps_rc, 4),
+            "stateful_ms_per_step": round(ms_per_step, 4),
+            "extra_us_per_step": round((t_rc / steps_rc - ms_per_step * 1e-3) * 1e6, 2),
+            "bwd_kernels_us": {k: round(u, 2) for k, u in kr.items()},
+            "bwd_graph_us": bwd_graph_us}
+        del g_rc, g_b, ws
+        step()
+        torch.cuda.synchronize()
+
+    # ---- leg: the single-output op's recompute-mode gradient (its extra cost over the stateful step)
+    if not args.no_recompute_leg:
+        leg("recompute_bwd", recompute_leg)
+
     def cold_leg():
         R = args.rotate
         rot = []
@@ -421,11 +499,19 @@ def main():
         from dirt_amd.sharding import gather_frames_to
         gather_frames_to(sess.pixels, batch, dst=0)
         t_root = timed(lambda: gather_frames_to(sess.pixels, batch, dst=0), n_g, barrier, world, device, shared)
+        # reduced-precision wire format: bf16 pixels, half the xGMI bytes
+        gather_frames_async(sess.pixels, batch, dtype=torch.bfloat16)[1]()
+        t_bf = timed(lambda: gather_frames_async(sess.pixels, batch, dtype=torch.bfloat16)[1](), n_g, barrier, world,
+                     device, shared)
+        t_root_bf = timed(lambda: gather_frames_to(sess.pixels, batch, dst=0, dtype=torch.bfloat16), n_g, barrier,
+                          world, device, shared)
         # pipelined: step k's frames move while step k+1 renders (two sessions, so a frame being gathered
         # is never overwritten; the step that reuses a session first waits for its gather)
         sess2 = RasteriseSession(B, H, W, C, V, F, device=device)
         pair = (sess, sess2)
         pend = [None, None]
+
+        mode = {"fn": lambda px: gather_frames_async(px, batch)}
 
         def piped(k):
             se = pair[k & 1]
@@ -433,7 +519,7 @@ def main():
                 pend[k & 1][0].wait()
             se.forward(bg, v, c, f)
             se.backward(grad)
-            pend[k & 1] = gather_frames_async(se.pixels, batch)
+            pend[k & 1] = mode["fn"](se.pixels)
 
         for k in range(4):
             piped(k)
@@ -454,6 +540,20 @@ def main():
                     p_[1]()
 
         t_p = timed(piped_all, 1, barrier, world, device, shared)
+        from dirt_amd.sharding import gather_frames_to_async
+        piped_modes = {}
+        for name, fn in (("bf16_all_gather", lambda px: gather_frames_async(px, batch, dtype=torch.bfloat16)),
+                         ("f32_to_rank0", lambda px: gather_frames_to_async(px, batch, dst=0)),
+                         ("bf16_to_rank0", lambda px: gather_frames_to_async(px, batch, dst=0, dtype=torch.bfloat16))):
+            mode["fn"] = fn
+            for k in range(4):
+                piped(k)
+            for p_ in pend:
+                p_[1]()
+            pend[:] = [None, None]
+            t_m = timed(piped_all, 1, barrier, world, device, shared)
+            piped_modes[name] = {"value_with_gather": round(world * B * H * W * args.steps / t_m / 1e6, 1),
+                                 "ms_per_step": round(t_m * 1e3 / args.steps, 4)}
         recv = (world - 1) * B * H * W * C * 4
         legs["gather"] = {
             "what": "all_gather_into_tensor of every rank's pixels [%d,%d,%d,%d] over %s per step" %
@@ -462,8 +562,11 @@ def main():
             "gather_to_rank0_ms": round(t_root * 1e3 / n_g, 4),
             "recv_bytes_per_rank": recv,
             "recv_GBps_per_rank": round(recv / (t_g / n_g) / 1e9, 1),
+            "gather_bf16_ms": round(t_bf * 1e3 / n_g, 4),
+            "gather_to_rank0_bf16_ms": round(t_root_bf * 1e3 / n_g, 4),
             "value_with_gather": round(world * B * H * W * args.steps / t_p / 1e6, 1),
-            "ms_per_step_with_gather": round(t_p * 1e3 / args.steps, 4)}
+            "ms_per_step_with_gather": round(t_p * 1e3 / args.steps, 4),
+            "pipelined_variants": piped_modes}
 
     # ---- leg (N > 1): the output all-gather over RCCL / xGMI, alone and overlapped with the next step
     if world > 1 and not args.no_gather_leg:

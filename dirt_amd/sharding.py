@@ -22,10 +22,22 @@ def shard_bounds(batch, rank, world):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def gather_frames(local, batch, group=None):
+def _wire(local, dtype):
+    """The block as it travels: `local` itself, or cast to the reduced-precision `dtype` (torch.bfloat16 /
+    torch.float16: half the xGMI bytes of float32 pixels; the gathered batch keeps that dtype)."""
+    if dtype is None or dtype == local.dtype:
+        return local
+    if dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError("gather dtype must be None, torch.bfloat16 or torch.float16, got %r" % (dtype,))
+    return local.to(dtype)
+
+
+def gather_frames(local, batch, group=None, dtype=None):
     """All-gather per-rank frame blocks [b_r, ...] into the full batch [batch, ...] on every rank.
 
-    Pads every block to the largest shard so one all_gather (RCCL ring over xGMI) moves it."""
+    Pads every block to the largest shard so one all_gather (RCCL ring over xGMI) moves it.  dtype:
+    optional reduced-precision wire format (see _wire)."""
+    local = _wire(local, dtype)
     world = dist.get_world_size(group)
     sizes = [shard_bounds(batch, r, world) for r in range(world)]
     mx = max(hi - lo for lo, hi in sizes)
@@ -36,11 +48,21 @@ def gather_frames(local, batch, group=None):
     return torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
 
 
-def gather_frames_to(local, batch, dst=0, group=None):
+def gather_frames_to(local, batch, dst=0, group=None, dtype=None):
     """Gather per-rank frame blocks into the full batch on rank `dst` only ("ncclGather to rank 0 if
     only one consumer"); returns the batch on `dst` and None on the other ranks.  Every rank sends its block
     once (RCCL send / recv over xGMI with the "nccl" backend); the root's ingress bounds it like the
-    all-gather's per-rank ingress, but the other ranks receive nothing."""
+    all-gather's per-rank ingress, but the other ranks receive nothing.  dtype: optional
+    reduced-precision wire format (see _wire)."""
+    work, finish = gather_frames_to_async(local, batch, dst=dst, group=group, dtype=dtype)
+    return finish()
+
+
+def gather_frames_to_async(local, batch, dst=0, group=None, dtype=None):
+    """gather_frames_to started asynchronously: returns (work, finish); finish() -> the batch on `dst`, None
+    elsewhere.  For a pipelined single consumer: the next step renders while this step's frames move to the
+    root."""
+    local = _wire(local, dtype)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     sizes = [shard_bounds(batch, r, world) for r in range(world)]
@@ -53,19 +75,26 @@ def gather_frames_to(local, batch, dst=0, group=None):
     via_host = pad.is_cuda and dist.get_backend(group) == "gloo"  # gloo moves host memory only
     src = pad.cpu() if via_host else pad
     outs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
-    dist.gather(src, gather_list=outs, dst=dst, group=group)
-    if rank != dst:
-        return None
-    full = torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
-    return full.to(local.device) if via_host else full
+    work = dist.gather(src, gather_list=outs, dst=dst, group=group, async_op=True)
+
+    def finish():
+        work.wait()
+        if rank != dst:
+            return None
+        full = torch.cat([o[: hi - lo] for o, (lo, hi) in zip(outs, sizes)], 0)
+        return full.to(local.device) if via_host else full
+
+    return work, finish
 
 
-def gather_frames_async(local, batch, group=None):
+def gather_frames_async(local, batch, group=None, dtype=None):
     """Start gathering per-rank frame blocks; returns (work, finish) where finish() -> the full batch.
 
     The collective runs on the backend's own stream (RCCL: its NCCL stream, which waits for the work
     already queued on the current stream), so the caller can queue the next step's render while the
-    frames move over xGMI; work.wait() makes the current stream wait for the gather."""
+    frames move over xGMI; work.wait() makes the current stream wait for the gather.  dtype: optional
+    reduced-precision wire format (see _wire; the cast is queued on the current stream)."""
+    local = _wire(local, dtype)
     world = dist.get_world_size(group)
     sizes = [shard_bounds(batch, r, world) for r in range(world)]
     mx = max(hi - lo for lo, hi in sizes)
@@ -115,13 +144,14 @@ def shared_across_ranks(x, group=None):
 
 
 def rasterise_batch_sharded(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
-                            channels=None, group=None, gather=False, render=rasterise_batch):
+                            channels=None, group=None, gather=False, render=rasterise_batch, gather_dtype=None):
     """rasterise_batch over this rank's contiguous share of the frames.
 
     Every rank passes the full batch (or any object supporting slicing on dim 0); the rank renders
     frames [lo, hi) and returns (pixels_local, (lo, hi)), or the gathered full batch if `gather`.
     Gradients flow through pixels_local like rasterise_batch; the gathered tensor is forward-only.
-    `render` is the per-shard renderer (the HIP op by default)."""
+    `render` is the per-shard renderer (the HIP op by default); `gather_dtype` the optional reduced-precision
+    wire format of the gather (torch.bfloat16 / torch.float16)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     B = background.shape[0]
@@ -131,6 +161,6 @@ def rasterise_batch_sharded(background, vertices, vertex_colors, faces, camera_p
     if not gather:
         return local, (lo, hi)
     if world == 1:
-        return local.detach()
+        return _wire(local.detach(), gather_dtype)
     with torch.no_grad():
-        return gather_frames(local.detach(), B, group=group)
+        return gather_frames(local.detach(), B, group=group, dtype=gather_dtype)

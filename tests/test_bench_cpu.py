@@ -27,3 +27,12 @@ def test_configs_and_host_info():
     info = bench.host_cpu_info()
     assert set(info) == {"cpu_model", "nproc_online", "affinity_cpus"} and info["affinity_cpus"] >= 1
     assert bench.cpu_threads() >= 1
+
+
+def test_cpu_share_evidence():
+    """The CPU baseline records where its thread count comes from (SURVEY 8d asks for all host cores; the pool
+    grants one GPU's job a share, OMP_NUM_THREADS on the box): cgroup quota / cpuset when readable."""
+    share = bench.cpu_share()
+    assert "OMP_NUM_THREADS" in share and share["nproc_online"] >= 1
+    if "cgroup_cpu_max" in share and share["cgroup_cpu_max"].split()[0] != "max":
+        assert share["cgroup_cpu_quota_cpus"] > 0

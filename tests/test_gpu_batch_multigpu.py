@@ -54,8 +54,8 @@ def _free_port():
 
 def _nccl_worker(port, inputs, outq):
     import torch.distributed as dist
-    from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, rasterise_batch_sharded,
-                                   shared_across_ranks)
+    from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, gather_frames_to_async,
+                                   rasterise_batch_sharded, shared_across_ranks)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -69,6 +69,12 @@ def _nccl_worker(port, inputs, outq):
         full3 = rasterise_batch_sharded(bg, v, c, f, gather=True)
         full4 = gather_frames_to(local, bg.shape[0], dst=0)  # RCCL gather to one root
         assert full.is_cuda and full2.is_cuda and full4.is_cuda
+        # reduced-precision wire formats over RCCL (half the xGMI bytes) and the async root gather
+        red = [gather_frames(local, bg.shape[0], dtype=torch.bfloat16),
+               gather_frames_async(local, bg.shape[0], dtype=torch.bfloat16)[1](),
+               gather_frames_to_async(local, bg.shape[0], dst=0, dtype=torch.float16)[1](),
+               gather_frames_to_async(local, bg.shape[0], dst=0)[1]()]
+        assert [t.dtype for t in red] == [torch.bfloat16, torch.bfloat16, torch.float16, torch.float32]
         # a parameter shared by the rank's frames: all_reduce over RCCL (world 1: the identity)
         x = torch.arange(6, dtype=torch.float32, device=dev).requires_grad_(True)
         (shared_across_ranks(x) * 2.0).sum().backward()
@@ -77,7 +83,7 @@ def _nccl_worker(port, inputs, outq):
         dist.all_reduce(y)
         torch.cuda.synchronize()
         outq.put((lo, hi, full.cpu().numpy(), full2.cpu().numpy(), full3.cpu().numpy(), full4.cpu().numpy(),
-                  x.grad.cpu().numpy(), float(y.sum())))
+                  x.grad.cpu().numpy(), float(y.sum()), [t.float().cpu().numpy() for t in red]))
     finally:
         dist.destroy_process_group()
 
@@ -99,12 +105,16 @@ def test_rccl_world1_gather_and_allreduce_on_device():
             if not p.is_alive():
                 break
     assert res is not None, "nccl worker exited with %s" % p.exitcode
-    lo, hi, full, full2, full3, full4, xgrad, ysum = res
+    lo, hi, full, full2, full3, full4, xgrad, ysum, red = res
     p.join(timeout=120)
     assert p.exitcode == 0
     assert (lo, hi) == (0, 3)
-    for a in (full, full2, full3, full4):
+    for a in (full, full2, full3, full4, red[3]):
         np.testing.assert_array_equal(a, ref)
+    rt = torch.from_numpy(ref)
+    np.testing.assert_array_equal(red[0], rt.bfloat16().float().numpy())
+    np.testing.assert_array_equal(red[1], rt.bfloat16().float().numpy())
+    np.testing.assert_array_equal(red[2], rt.half().float().numpy())
     np.testing.assert_array_equal(xgrad, np.full(6, 2.0, np.float32))
     assert ysum == 1000.0
 

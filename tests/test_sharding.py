@@ -14,8 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import scenes
-from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, rasterise_batch_sharded,
-                               shard_bounds, shared_across_ranks)
+from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, gather_frames_to_async,
+                               rasterise_batch_sharded, shard_bounds, shared_across_ranks)
 from oracle import oracle
 
 
@@ -57,11 +57,21 @@ def _worker(rank, world, port, inputs, outq):
         full3 = finish()
         root = gather_frames_to(local, bg.shape[0], dst=1)  # the single-consumer gather: rank 1 only
         root = None if root is None else root.numpy()
+        # reduced-precision wire formats (half the xGMI bytes): every path returns the cast batch
+        red = {}
+        for dt in (torch.bfloat16, torch.float16):
+            a = gather_frames(local, bg.shape[0], dtype=dt)
+            b = gather_frames_async(local, bg.shape[0], dtype=dt)[1]()
+            r0 = gather_frames_to_async(local, bg.shape[0], dst=0, dtype=dt)[1]()
+            g2 = rasterise_batch_sharded(bg, v, c, f, render=_oracle_render, gather=True, gather_dtype=dt)
+            assert a.dtype == b.dtype == g2.dtype == dt and (r0 is None) == (rank != 0)
+            red[str(dt)] = (a.float().numpy(), b.float().numpy(), None if r0 is None else r0.float().numpy(),
+                            g2.float().numpy())
         # a parameter shared by every rank's frames: its gradient is summed over the ranks
         x = torch.arange(6, dtype=torch.float32).requires_grad_(True)
         loss = (shared_across_ranks(x) * (rank + 1)).sum() + (x * x).sum() * 0.0
         loss.backward()
-        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy(), full3.numpy(), x.grad.numpy(), root))
+        outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy(), full3.numpy(), x.grad.numpy(), root, red))
     finally:
         dist.destroy_process_group()
 
@@ -82,7 +92,13 @@ def test_two_rank_sharded_batch_matches_single_process(B):
         assert p.exitcode == 0
     res.sort(key=lambda r: r[0])
     covered = []
-    for rank, lo, hi, local, full, full2, full3, xgrad, root in res:
+    for rank, lo, hi, local, full, full2, full3, xgrad, root, red in res:
+        for dt in (torch.bfloat16, torch.float16):
+            want = torch.from_numpy(ref).to(dt).float().numpy()
+            for k, got in enumerate(red[str(dt)]):
+                if got is not None:
+                    np.testing.assert_array_equal(got, want)
+        assert red[str(torch.bfloat16)][2] is not None if rank == 0 else red[str(torch.bfloat16)][2] is None
         np.testing.assert_array_equal(full3, ref)          # the async all_gather_into_tensor path
         if rank == 1:
             np.testing.assert_array_equal(root, ref)       # gather to one root reassembles the batch there
