@@ -452,13 +452,14 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
         zero2_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(grad_vertices, na, grad_vertex_colors, nb);
         HIP_TRY(hipGetLastError());
     }
-    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+    // backward tiles: kGradTileW x 16 (grad_kernel.h)
+    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + kGradTileH - 1) / kGradTileH;
+    dim3 grid((unsigned)(gntx * gnty), (unsigned)B);
     ProfScope ps(K_GRAD, stream);
 #define LAUNCH_GRAD(CC)                                                                                       \
-    grad_kernel<CC><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, \
-                                                    V, F,                                                        \
-                                                    tile_grid(L.ntx), L.nrec, grad_vertices, grad_vertex_colors,            \
-                                                    grad_background, ndc_scale(W, H))
+    grad_kernel<CC><<<grid, dim3(GradGeom<kGradTileW>::NT), 0, stream>>>(                                      \
+        pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,          \
+        grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H))
     if (C == 1) LAUNCH_GRAD(1);
     else if (C == 3) LAUNCH_GRAD(3);
     else if (C == 7) LAUNCH_GRAD(7);
@@ -639,17 +640,18 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, stream));
-    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + kGradTileH - 1) / kGradTileH;
+    dim3 grid((unsigned)(gntx * gnty), (unsigned)B), blk(GradGeom<kGradTileW>::NT);
 #define V_GRAD(AB)                                                                                                   \
     case AB:                                                                                                         \
         if (C == 3)                                                                                                  \
-            grad_kernel<3, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, \
-                                                               H, W, C, V, F, tile_grid(L.ntx), L.nrec, grad_vertices, \
-                                                               grad_vertex_colors, grad_background, ndc_scale(W, H));  \
+            grad_kernel<3, AB><<<grid, blk, 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B,       \
+                                                         H, W, C, V, F, tile_grid(gntx), L.nrec, grad_vertices,       \
+                                                         grad_vertex_colors, grad_background, ndc_scale(W, H));       \
         else                                                                                                         \
-            grad_kernel<7, AB><<<grid, dim3(256), 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, \
-                                                               H, W, C, V, F, tile_grid(L.ntx), L.nrec, grad_vertices, \
-                                                               grad_vertex_colors, grad_background, ndc_scale(W, H));  \
+            grad_kernel<7, AB><<<grid, blk, 0, stream>>>(pixels, grad_pixels, gbuffer, covbits, recs, fdata, B,       \
+                                                         H, W, C, V, F, tile_grid(gntx), L.nrec, grad_vertices,       \
+                                                         grad_vertex_colors, grad_background, ndc_scale(W, H));       \
         break
     switch (variant) {
         V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);

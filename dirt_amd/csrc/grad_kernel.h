@@ -4,7 +4,7 @@
 // ------------------------------------------------------------------------------------------------
 // K5: backward
 //
-// One 256-thread workgroup per 16x16 tile, one lane per pixel.  Every contribution of a lane goes to
+// One workgroup per TWX x 16 tile (TWX = 16: 256 threads, TWX = 32: 512), one lane per pixel.  Every contribution of a lane goes to
 // the face visible at its own pixel: colour gradients lambda_k * G, and the share of the four
 // neighbour pairs around the pixel that this face owns (a pair's other owner is handled by the lane
 // on the other side, same-face pairs by the lower lane only).  Reduction without global contention:
@@ -101,8 +101,21 @@ struct NdcScale {
     float inv_hw, inv_hh, half_w, half_h;
 };
 
-constexpr int kHalo = kTile + 2;   // staged tile with a one-pixel border
-constexpr int kHaloPix = kHalo * kHalo;
+// Backward tile width: 16 (16x16 tiles, 256-thread workgroups) or 32 (32x16, 512 threads: 1.20 instead of
+// 1.27 staged pixels per pixel, and records spanning both halves are inserted, loaded and flushed once).
+#ifndef DIRT_GRAD_TILE_W
+#define DIRT_GRAD_TILE_W 16
+#endif
+constexpr int kGradTileW = DIRT_GRAD_TILE_W;
+constexpr int kGradTileH = 16;
+// staged tile with a one-pixel border: row stride TWX + 2, 18 rows
+template <int TWX>
+struct GradGeom {
+    static constexpr int NT = TWX * kGradTileH;   // threads
+    static constexpr int HX = TWX + 2;            // staged row stride
+    static constexpr int HY = kGradTileH + 2;
+    static constexpr int PIX = HX * HY;
+};
 constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS (typ. 10-40)
 constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
 static_assert(kSlots <= 128, "slot ids (0 .. kSlots-1) are stored as int8");
@@ -124,8 +137,8 @@ struct SlotTable {
 
 // A record is "small" for the backward when every |A|, |B| < 2^14 (edges shorter than 64 px).  Such a
 // record is visible somewhere in the 18x18 tile + halo region, so at every region pixel its edge values
-// satisfy |E| < 2^28 (E at a covered pixel) + 2 * 2^14 * 17 * 256 < 2^30: exact in int32, and a
-// coverage test is E0 + A*256*hx + B*256*hy with 24-bit multiplies (hx, hy in 0..17).
+// satisfy |E| < 2^28 (E at a covered pixel) + 2 * 2^14 * 33 * 256 < 2^30: exact in int32, and a
+// coverage test is E0 + A*256*hx + B*256*hy with 24-bit multiplies (hx in 0..33, hy in 0..17).
 constexpr int32_t kGradSmallEdge = 1 << 14;
 constexpr uint32_t kSlotLarge = 0x80000000u;
 
@@ -216,7 +229,7 @@ __device__ __forceinline__ float pair_scalar(const int32_t *s_gb, const float *s
 }
 
 // Index (0..15) of the first lane of this lane's run of equal `key` in its 16-lane DPP row.
-__device__ __forceinline__ int run_start(int key, int lx)
+__device__ __forceinline__ int run_start(int key, int lx)  // lx: lane index within its 16-lane DPP row
 {
     const int kl = dpp_shr_i<1>(key, -3);
     int start = (lx == 0 || kl != key) ? lx : -1;
@@ -231,8 +244,8 @@ __device__ __forceinline__ int run_start(int key, int lx)
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
 // 32 skip the DPP run scan (every lane adds into LDS), 128 phase timestamps, 256 flush sums without
 // the global atomics
-template <int CC, int AB = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
+template <int CC, int AB = 0, int TWX = kGradTileW>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
                           amdgpu_waves_per_eu(CC == 3 ? DIRT_GRAD_WAVES_C3 : DIRT_GRAD_WAVES))) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
                                                    const Rec *__restrict__ recs,
@@ -242,6 +255,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
                                                    const NdcScale ns)
 {
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
+    constexpr int NT = GradGeom<TWX>::NT, kHalo = GradGeom<TWX>::HX, kHaloPix = GradGeom<TWX>::PIX;
     // LDS pixel stride: float4 for RGB, two float4 for 5..8 channels (wide LDS reads)
     constexpr int CP = CM == 3 ? 4 : (CM > 4 && CM <= 8) ? 8 : CM;
     constexpr int NVM = 9 + 3 * CM;
@@ -287,8 +301,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     const int tile = xcd_tile(blockIdx.x, gridDim.x), b = blockIdx.y;
     int tx, ty;
     tg.split(tile, tx, ty);
-    const int t = threadIdx.x, lx = t & 15, ly = t >> 4;
-    const int i = tx * kTile + lx, j = ty * kTile + ly;
+    const int t = threadIdx.x, lx = t % TWX, ly = t / TWX;
+    const int lr = lx & 15;  // lane within its 16-lane DPP row (a pixel row, or half of one at TWX = 32)
+    const int i = tx * TWX + lx, j = ty * kGradTileH + ly;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
     // uniform: readfirstlane (convergent) keeps the divisions at the top instead of in every pair branch
@@ -298,15 +313,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
 
     // ---- phase A: stage g-buffer / G / I of the tile + one-pixel halo, pair scalars, slot table
     PHASE_TS(0);
-    for (int k = t; k < kSlots; k += 256) {
+    for (int k = t; k < kSlots; k += NT) {
         T.key[k] = -1;
         s_tcnt[k] = 0;
     }
     if (t == 0) T.n = 0;
-    const int hi0 = tx * kTile - 1, hj0 = ty * kTile - 1;
+    const int hi0 = tx * TWX - 1, hj0 = ty * kGradTileH - 1;
     {
-        // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * 256)
-        static_assert(kHaloPix <= 512, "two staging passes");
+        // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * NT)
+        static_assert(kHaloPix <= 2 * NT, "two staging passes");
         // frame base pointers (64-bit, uniform) + 32-bit per-lane offsets: H * W * C < 2^29
         const int64_t fpix = (int64_t)b * H * W;
         const int32_t *gb_f = gbuffer + fpix;
@@ -318,7 +333,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         bool ok[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int k = t + 256 * u;
+            const int k = t + NT * u;
             const int hi = hi0 + k % kHalo, hj = hj0 + k / kHalo;
             ok[u] = k < kHaloPix && hi >= 0 && hj >= 0 && hi < W && hj < H;
             gbv[u] = -2;
@@ -340,7 +355,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int k = t + 256 * u;
+            const int k = t + NT * u;
             if (k >= kHaloPix) continue;
             // a background pixel with a non-finite value (G-buffers rendered over -inf,
             // samples/deferred.py:67,81) defines no image difference: staged as "outside the frame", so
@@ -388,9 +403,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         // memory).  The halo's records are not needed: pair coverage comes from the forward's bits.
         const int32_t g = s_gb[kme];
         const int key = g >= 0 ? g : -1;
-        const int start = run_start(key, lx);
-        int slot = slot_insert_wave(T, key, key >= 0 && start == lx);
-        if (key >= 0 && start == lx && slot >= 0) atomicAdd(&s_tcnt[slot], 1);  // one run (one tail later)
+        const int start = run_start(key, lr);
+        int slot = slot_insert_wave(T, key, key >= 0 && start == lr);
+        if (key >= 0 && start == lr && slot >= 0) atomicAdd(&s_tcnt[slot], 1);  // one run (one tail later)
         slot = __shfl(slot, (t & 48) + start, 64);
         s_slot[kme] = key >= 0 ? slot : -1;
     }
@@ -436,11 +451,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         if constexpr (!kRecompute) {
         s_sx[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + 1, C);
         s_sy[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + kHalo, C);
-        if (t >= 224) {
-            // the 32 halo pairs into the tile, one per lane of the last wave and one pair_scalar for all
-            // of them (the LDS reads of a pair are wide: spreading them over every wave, or a branch per
+        if (t >= NT - 64 && t - (NT - 64) < 16 + TWX) {
+            // the 16 + TWX halo pairs into the tile, one per lane of the last wave and one pair_scalar for
+            // all of them (the LDS reads of a pair are wide: spreading them over every wave, or a branch per
             // axis, would cost each wave two more rounds of them)
-            const int h = t - 224;
+            const int h = t - (NT - 64);
             const bool xa = h < 16;
             const int k = xa ? (h + 1) * kHalo : h - 15;  // (0, h + 1) or (h - 15, 0)
             const float sv = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + (xa ? 1 : kHalo), C);
@@ -651,27 +666,31 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
             const float ndc = mid * (axis == 0 ? inv_hw : inv_hh) - 1.0f;
             // lambda_k / Wm = a_k / sum_k (a_k w_k) = a_k / (2E_0 + 2E_1 + 2E_2 + st_0 + st_1 + st_2) = a_k / (2D)
             // (iw_k w_k = 1, the edge functions sum to the constant D and their steps to 0): no division per
-            // pair and nothing to cancel.  A clipped face's sub-triangle maps the same weights of its own
-            // vertices through the clip basis to the parent's: its vertices are convex combinations of the
-            // parent's (w_sub = basis . w), so parent lambda_i / Wm = sum_k a_k basis_ki / (2D) of the
-            // sub-triangle -- the normalised form lambda = a / sum a, Wm = sum lambda w cancelled
-            // on slivers.
+            // pair and nothing to cancel.  For a clipped face these are the weights of its sub-triangle's
+            // vertices; they are mapped to the parent's below, once per pixel.
             const float c = omega * s * half * h2d;
-            float g[3];
-            if (!multi) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) g[k] = c * m[k];
-            } else {
-                const Rec &rr = rec();
-#pragma unroll
-                for (int k = 0; k < 3; ++k)
-                    g[k] = c * ((m[0] * rr.basis[k] + m[1] * rr.basis[3 + k]) + m[2] * rr.basis[6 + k]);
-            }
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                acc[k * 3 + axis] += g[k];
-                acc[k * 3 + 2] -= g[k] * ndc;
+                const float g = c * m[k];
+                acc[k * 3 + axis] += g;
+                acc[k * 3 + 2] -= g * ndc;
             }
+        }
+        if (multi) {
+            // A clipped face's sub-triangle has vertices that are convex combinations of the parent's (the
+            // clip basis rows; w_sub = basis . w), so the parent's lambda_i / Wm = sum_k basis_ki a_k / (2D)
+            // (the normalised form lambda = a / sum a, Wm = sum lambda w cancelled on slivers).
+            // Linear in the weights: the pixel's accumulated sub-vertex sums are mapped once, all pairs of
+            // a lane being owned by its own record.
+            const Rec &rr = rec();
+            float sub[9];
+#pragma unroll
+            for (int v = 0; v < 9; ++v) sub[v] = acc[v];
+#pragma unroll
+            for (int i2 = 0; i2 < 3; ++i2)
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    acc[i2 * 3 + a] = (rr.basis[i2] * sub[a] + rr.basis[3 + i2] * sub[3 + a]) + rr.basis[6 + i2] * sub[6 + a];
         }
         }
         // colour weights last: keeps their registers out of the pair loop's live range
@@ -698,11 +717,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     // (sized in phase A by counting run heads; LDS float atomics serialise on shared addresses); tails
     // without a slot (table full) or past the partial buffer add straight to global memory
     const int key = rp >= 0 ? rp : -1;
-    const int start = run_start(key, lx);
+    const int start = run_start(key, lr);
     // 0/1 multipliers: x += shifted(x) * m is one v_fmac with a DPP operand (exact: m is 0 or 1,
     // contributions are finite)
-    const float mk1 = lx - 1 >= start ? 1.0f : 0.0f, mk2 = lx - 2 >= start ? 1.0f : 0.0f;
-    const float mk4 = lx - 4 >= start ? 1.0f : 0.0f, mk8 = lx - 8 >= start ? 1.0f : 0.0f;
+    const float mk1 = lr - 1 >= start ? 1.0f : 0.0f, mk2 = lr - 2 >= start ? 1.0f : 0.0f;
+    const float mk4 = lr - 4 >= start ? 1.0f : 0.0f, mk8 = lr - 8 >= start ? 1.0f : 0.0f;
     if (!(AB & 32)) {
         // step-major order: each v_fmac_f32_dpp reads a register written >= NVM-1 instructions
         // earlier (no DPP read-after-write hazard inside the asm)
@@ -717,7 +736,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
         for (int v = 0; v < NVM; ++v) asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:8 bound_ctrl:0" : "+v"(acc[v]) : "v"(mk8));
     }
     const int kr = dpp_shl_i<1>(key, -3);
-    const bool tail = key >= 0 && ((AB & 32) || lx == 15 || kr != key);
+    const bool tail = key >= 0 && ((AB & 32) || lr == 15 || kr != key);
     float *gvb = grad_verts + (int64_t)b * V * 4;
     float *gcb = grad_colors + (int64_t)b * V * C;
     __syncthreads();  // every read of s_G / s_I is done: the union now holds tail partials
@@ -752,7 +771,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256),
     const int n = (AB & 8) ? 0 : nslots;
     // whole records per wave: no record's components straddle two waves, so each record's atomics leave
     // in one wave instruction (the cache lines one atomic instruction touches are what it costs)
-    const int rpw = 64 / NV, per_round = 4 * rpw;
+    const int rpw = 64 / NV, per_round = (NT / 64) * rpw;
     const int wl = t & 63;
     for (int e0 = 0; e0 < n; e0 += per_round) {
         const int e = e0 + (t >> 6) * rpw + wl / NV, comp_id = wl - (wl / NV) * NV;
