@@ -120,7 +120,10 @@ constexpr int kMaxCoarse = 4096;   // LDS histogram size in setup
 #define DIRT_BIN_THREADS 256
 #endif
 constexpr int kBinThreads = DIRT_BIN_THREADS;
-constexpr int64_t kDefaultBinBudget = 1ll << 27;  // entries (1 GiB) above which the default slab shrinks
+// entries (4 GiB of the 288 GB HBM) above which the default slab shrinks: B = 64 frames of 1024^2 and 20k faces
+// (config 5 on one GPU) keep the full F + F/4 + 64 per slab, so a mesh crowded into a few coarse tiles does
+// not send them to the overflow path (dirt_debug_bin_occupancy reports the fullest slab)
+constexpr int64_t kDefaultBinBudget = 1ll << 29;
 // Count-set parity, so that no kernel has to return the counts it read to zero.  Words of the flag area
 // (separate 64-B lines): [0] out-of-range-face flag, [kParP] P, [kParQ] Q.  The setup kernel reads p = Q,
 // publishes P = p, accumulates into counts[p] and zeroes counts[p ^ 1] (read by the previous forward's
@@ -528,6 +531,45 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
     if (rc) return rc;
     return dirt_rasterise_bwd(vertices, vertex_colors, faces, pixels, grad_pixels, gbuf, ws, B, H, W, C, V, F,
                               grad_vertices, grad_vertex_colors, grad_background, DIRT_BWD_ACCUMULATE, stream_);
+}
+
+__global__ void bin_occupancy_kernel(const uint32_t *__restrict__ counts, int64_t nslabs, uint32_t slab, uint32_t *out)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nslabs; k += (int64_t)gridDim.x * blockDim.x) {
+        // this forward's count set holds the counts, the other set is zero (kParP)
+        const uint32_t n = counts[k * kCountStride] + counts[(nslabs + k) * kCountStride];
+        atomicMax(&out[0], n);
+        if (n > slab) atomicAdd(&out[1], 1u);
+    }
+}
+
+// Debug (synchronises `stream`): the bin occupancy the last forward left in `scratch` -- the fullest slab's
+// entry count, the number of slabs that overflowed (their tiles took the all-records path) and the slab
+// capacity.  Not part of include/dirt_mi355x.h.
+int dirt_debug_bin_occupancy(int B, int H, int W, int F, int64_t bin_capacity, const void *scratch,
+                             size_t scratch_bytes, void *stream_, uint32_t *max_count, uint32_t *overflowed,
+                             uint32_t *slab)
+{
+    Layout L;
+    int rc = make_layout(B, H, W, F, bin_capacity, L);
+    if (rc) return rc;
+    if (!scratch || scratch_bytes < L.scratch_total) return fail(DIRT_EINVAL, "dirt_debug_bin_occupancy: scratch too small");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    uint32_t *d = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&d), 8, stream));
+    HIP_TRY(hipMemsetAsync(d, 0, 8, stream));
+    const int64_t nslabs = (int64_t)B * L.ncoarse;
+    bin_occupancy_kernel<<<dim3(256), dim3(256), 0, stream>>>(
+        reinterpret_cast<const uint32_t *>(static_cast<const char *>(scratch) + L.off_count), nslabs, L.slab, d);
+    HIP_TRY(hipGetLastError());
+    uint32_t h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipFreeAsync(d, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (max_count) *max_count = h[0];
+    if (overflowed) *overflowed = h[1];
+    if (slab) *slab = L.slab;
+    return DIRT_OK;
 }
 
 // Ablation entry point (tools/ablate.py): re-runs raster_kernel (C == 3) on the bins a preceding

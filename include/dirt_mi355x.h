@@ -78,7 +78,7 @@ int dirt_abi_version(void);
 /* Byte sizes of the caller-provided buffers for one call.
  * bin_capacity = number of (coarse tile, triangle) bin entries the scratch can hold, split evenly into
  * one slab per (frame, coarse tile); <=0: default policy (F + F/4 + 64 entries per slab, so no slab of
- * a frame overflows unless many faces are clipped into one tile, up to 2^27 entries in all).  A slab
+ * a frame overflows unless many faces are clipped into one tile, up to 2^29 entries (4 GiB) in all).  A slab
  * that overflows is still rendered exactly, by a slow path that filters every record of the frame. */
 int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_capacity,
                          size_t *saved_bytes, size_t *scratch_bytes);

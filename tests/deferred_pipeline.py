@@ -48,16 +48,23 @@ def _camera_cpu(H, W):
     return view, proj, torch.linalg.inv(view)[3, :3]
 
 
+@functools.lru_cache(maxsize=16)
+def _camera_on(H, W, device):
+    view, proj, pos = _camera_cpu(H, W)
+    return view.to(device), proj.to(device), pos.to(device)
+
+
 def camera(H, W, device=None):
     """The sample's camera (samples/deferred.py:50-60, OpenGL perspective); the surface is tilted towards the
-    camera (rotation about x) and pushed away along -z.  Built once on the CPU, then moved."""
-    view, proj, _ = _camera_cpu(H, W)
-    return view.to(device), proj.to(device)
+    camera (rotation about x) and pushed away along -z.  Built once on the CPU, moved once per device (so a
+    step can be captured into a HIP graph: no host-to-device copy inside it)."""
+    view, proj, _ = _camera_on(H, W, torch.device(device) if device is not None else torch.device("cpu"))
+    return view, proj
 
 
 def camera_position(H, W, device=None):
     """The camera's world position, tf.matrix_inverse(view_matrix)[3, :3] (samples/deferred.py:107)."""
-    return _camera_cpu(H, W)[2].to(device)
+    return _camera_on(H, W, torch.device(device) if device is not None else torch.device("cpu"))[2]
 
 
 @functools.lru_cache(maxsize=16)

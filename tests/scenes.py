@@ -106,12 +106,13 @@ def cylinder_scene(W=48, H=36, seed=0, bgcolor=(0.4, 0.2, 0.2), vertex_color=(0.
     return bg.astype(np.float32), clip.detach().numpy().astype(np.float32), cols, faces.numpy().astype(np.int32)
 
 
-def random_triangles(F=50000, W=1024, H=1024, C=3, radius_px=16.0, seed=0, perspective=False):
+def random_triangles(F=50000, W=1024, H=1024, C=3, radius_px=16.0, seed=0, perspective=False, spread=1.0):
     """SURVEY 8d synthetic distribution (BASELINE config 3): centres U[-1,1]^2, vertex offsets uniform in a
     disk of radius `radius_px` pixels, z ~ U(-0.95,0.95) +-0.01 jitter, w=1 (or w~U(1,3) scaling xyz);
-    split vertices (V=3F), colours and background U[0,1]."""
+    split vertices (V=3F), colours and background U[0,1].  spread < 1: centres U[-spread, spread]^2 (a
+    clustered mesh: spread 0.25 puts every face in the centre 1/16 of the frame)."""
     rng = np.random.default_rng(seed)
-    centres = rng.uniform(-1, 1, size=(F, 1, 2))
+    centres = rng.uniform(-spread, spread, size=(F, 1, 2))
     ang = rng.uniform(0, 2 * np.pi, size=(F, 3))
     rad = radius_px * np.sqrt(rng.uniform(0, 1, size=(F, 3)))
     off = np.stack([np.cos(ang) * rad * 2.0 / W, np.sin(ang) * rad * 2.0 / H], -1)

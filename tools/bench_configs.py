@@ -29,7 +29,30 @@ CONFIGS = {
     "c5_batch8x20k_1024x1024x3_per_gpu": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024, seed=b)
                                                   for b in range(8)],
     "c3_stress_r64_1024x1024x3": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, radius_px=64.0, seed=0)],
+    # a mesh crowded into the centre 1/16 of each frame at config 5's per-rank batch, at the
+    # default bin capacity and with the slabs forced small (1024 entries: the crowded tiles overflow and take
+    # the all-records path), to price the overflow path
+    "c5_clustered_8x20k_centre16th": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024, seed=200 + b,
+                                                                      spread=0.25) for b in range(8)],
+    "c5_clustered_8x20k_centre16th_slab1024": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024,
+                                                                               seed=200 + b, spread=0.25)
+                                                       for b in range(8)],
 }
+# per-config bin capacity (entries in all slabs; 0 = default)
+BIN_CAPACITY = {"c5_clustered_8x20k_centre16th_slab1024": 8 * 256 * 1024}
+
+
+def bin_occupancy(B, H, W, F, cap, scratch, nbytes):
+    import ctypes
+    lib = _lib.load()
+    fn = lib.dirt_debug_bin_occupancy
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int] * 4 + [ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p] + \
+        [ctypes.POINTER(ctypes.c_uint32)] * 3
+    mx, ov, slab = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    _lib.check(fn(B, H, W, F, cap, scratch.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream,
+                  ctypes.byref(mx), ctypes.byref(ov), ctypes.byref(slab)))
+    return {"max_slab_entries": mx.value, "overflowed_slabs": ov.value, "slab_capacity": slab.value}
 
 
 def cpu_oracle(host, g, budget_s=3.0):
@@ -52,7 +75,9 @@ def cpu_oracle(host, g, budget_s=3.0):
 
 def deferred_chain(steps=20):
     """c4 as the reference sample runs it: three 3-channel G-buffer renders + dilation + lighting + loss,
-    backward to world-space vertices (tests/deferred_pipeline.py), through dirt_amd.rasterise + autograd."""
+    backward to world-space vertices (tests/deferred_pipeline.py), through dirt_amd.rasterise + autograd.
+    Reported eager (host-issued every step), as one captured HIP graph per step (device time: the whole
+    chain replayed, no host work), and the host's issue time alone (eager wall time minus nothing queued)."""
     import deferred_pipeline as dp
     dev = torch.device("cuda", 0)
     H = W = 512
@@ -61,10 +86,11 @@ def deferred_chain(steps=20):
     f = torch.from_numpy(faces).to(dev)
     al = torch.from_numpy(albedo).to(dev)
     wts = torch.rand((H, W, 3), device=dev)
+    out = {}
 
     def step():
         L, _, _ = dp.chain(dp.hip_render, Vw, f, al, H, W, wts)
-        torch.autograd.grad(L, [Vw])
+        out["g"] = torch.autograd.grad(L, [Vw])[0]
 
     for _ in range(3):
         step()
@@ -74,8 +100,42 @@ def deferred_chain(steps=20):
         step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    return {"config": "c4_deferred_chain_3x512x512x3_grad_to_world_vertices", "faces": len(faces),
-            "ms_per_step_eager": round(dt * 1e3, 3), "Mpixels_per_s_fwd_bwd": round(H * W / dt / 1e6, 1)}
+    ref = out["g"].clone()
+    # host issue time: the same steps with the device already busy is what eager costs; time the Python /
+    # autograd work alone by issuing without synchronising and reading the host clock
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    t_issue = (time.perf_counter() - t0) / steps
+    torch.cuda.synchronize()
+    res = {"config": "c4_deferred_chain_3x512x512x3_grad_to_world_vertices", "faces": len(faces),
+           "ms_per_step_eager": round(dt * 1e3, 3), "host_issue_ms_per_step": round(t_issue * 1e3, 3),
+           "Mpixels_per_s_fwd_bwd": round(H * W / dt / 1e6, 1)}
+    try:
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            step()
+        graph.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            graph.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        dg = e0.elapsed_time(e1) / steps
+        err = float((out["g"] - ref).abs().max() / ref.abs().max())
+        res.update({"ms_per_step_graph": round(dg, 4), "Mpixels_per_s_graph": round(H * W / (dg * 1e-3) / 1e6, 1),
+                    "graph_grad_rel_diff_vs_eager": err})
+        del graph
+    except Exception as e:  # noqa: BLE001 -- reported, not fatal
+        res["graph_error"] = "%s: %s" % (type(e).__name__, str(e)[:200])
+    return res
 
 
 def run(name, frames, steps=100):
@@ -85,7 +145,8 @@ def run(name, frames, steps=100):
     B, H, W, C = bg.shape
     V, F = v.shape[1], f.shape[1]
     g = torch.randn((B, H, W, C), device=dev)
-    sess = RasteriseSession(B, H, W, C, V, F, device=dev)
+    cap = BIN_CAPACITY.get(name, 0)
+    sess = RasteriseSession(B, H, W, C, V, F, device=dev, bin_capacity=cap)
 
     def step():
         sess.forward(bg, v, c, f)
@@ -93,6 +154,9 @@ def run(name, frames, steps=100):
 
     for _ in range(5):
         step()
+    sess.forward(bg, v, c, f)
+    occ = bin_occupancy(B, H, W, F, cap, sess.scratch, sess.scratch_bytes)
+    sess.backward(g)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         for _ in range(10):
@@ -112,7 +176,7 @@ def run(name, frames, steps=100):
     _lib.profile_enable(False)
     out = {"config": name, "frames": B, "H": H, "W": W, "C": C, "faces": F, "vertices": V,
            "Mpixels_per_s_fwd_bwd": round(B * H * W / dt / 1e6, 1), "us_per_step": round(dt * 1e6, 2),
-           "kernels_us": {k: round(ms / n * 1e3, 2) for k, (n, ms) in prof.items() if n}}
+           "kernels_us": {k: round(ms / n * 1e3, 2) for k, (n, ms) in prof.items() if n}, "bins": occ}
     if os.environ.get("DIRT_NO_CPU") != "1":
         out.update(cpu_oracle(host, g.cpu().numpy()))
         out["gpu_over_cpu"] = round(out["Mpixels_per_s_fwd_bwd"] / max(out["cpu_Mpixels_per_s"], 1e-9), 1)
