@@ -68,6 +68,16 @@ inline TileGrid tile_grid(int ntx) { return TileGrid{ntx, (uint32_t)(((1ull << 3
 #ifndef DIRT_RASTER_HZ_MIN
 #define DIRT_RASTER_HZ_MIN 32
 #endif
+// Occluder culling before the entry loop (depth-tested programs): a wave whose list holds more than
+// DIRT_RASTER_OCC_MIN entries first bounds its block's final depth by the nearest entry that covers the whole
+// block (entry_occluder_qmax), then drops every entry whose depth lower bound exceeds it -- in deep scenes
+// (large overlapping triangles) most of the list, before any of it runs.  Results are bit-identical.
+#ifndef DIRT_RASTER_OCC
+#define DIRT_RASTER_OCC 1
+#endif
+#ifndef DIRT_RASTER_OCC_MIN
+#define DIRT_RASTER_OCC_MIN 32
+#endif
 constexpr int kWaveList = 256 + 2;  // a staging round's entries + the even pad
 constexpr int kFilterBlock = 128;  // coarse-bin entries filtered per wave and chunk (2 loads per lane in flight)
 // A staged record is "small" when every |A|, |B| < 2^15: its edge steps inside a strip are one
@@ -259,6 +269,55 @@ __device__ __forceinline__ uint32_t entry_qmin(const StripEntry *ent, uint32_t o
     return zq > 0.0f ? (uint32_t)fminf(zq, 16777215.0f) : 0u;
 }
 #endif
+
+// Occluder bound (DIRT_RASTER_OCC): a staged small entry that covers the wave's whole 8x8 block (all four
+// corner pixel centres inside -- the block is convex) with its depth inside [0, 1) there writes or beats every
+// pixel of the block, so every final key of the block has depth <= this entry's maximum there.  Returns a
+// conservative upper bound of that maximum (the plane at the corner its slopes point to, plus twice the
+// two-rounding error bound and two quanta), or 0xffffffff when the entry is not such an occluder.
+__device__ __forceinline__ uint32_t entry_occluder_qmax(const StripEntry *ent, uint32_t off, int bx, int by, int x0,
+                                                        int y0)
+{
+    lds_int4v *ve = (lds_int4v *)((const char *)ent + off);
+    const int cx0 = 256 * bx, cx1 = 256 * (bx + kWaveW - 1), cy0 = 256 * by, cy1 = 256 * (by + kWaveH - 1);
+    // two rounds of (volatile, so ordered) LDS reads: the coverage half first, then the depth plane -- fewer
+    // registers live at once than one batch of three b128 reads
+    bool cover = true;
+    {
+        const int4v q0 = ve[0], q1 = ve[1];
+        const int e[3] = {q0.x, q0.y, q0.z};
+        const uint32_t ab[3] = {(uint32_t)q0.w, (uint32_t)q1.x, (uint32_t)q1.y};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int A = (int)(short)(ab[k] & 0xffffu), B = (int)(short)(ab[k] >> 16);
+            // the edge function is linear: its minimum over the block is at a corner (E + owned > 0 = inside)
+            cover = cover && e[k] + min(A * cx0, A * cx1) + min(B * cy0, B * cy1) > 0;
+        }
+    }
+    const int4v q1 = ve[1], q2 = ve[2];
+    const float za = __int_as_float(q1.z), zb = __int_as_float(q1.w), z0 = __int_as_float(q2.w);
+    const float xa = (float)x0 + 0.5f - __int_as_float(q2.x), xb = (float)(x0 + kWaveW - 1) + 0.5f - __int_as_float(q2.x);
+    const float ya = (float)y0 + 0.5f - __int_as_float(q2.y), yb = (float)(y0 + kWaveH - 1) + 0.5f - __int_as_float(q2.y);
+    const float zhi = depth_at(za, zb, z0, za > 0.0f ? xb : xa, zb > 0.0f ? yb : ya);
+    const float zlo = depth_at(za, zb, z0, za > 0.0f ? xa : xb, zb > 0.0f ? ya : yb);
+    const float m = (fabsf(za) * fmaxf(fabsf(xa), fabsf(xb)) + fabsf(zb) * fmaxf(fabsf(ya), fabsf(yb)) + fabsf(z0)) * 0x1p-21f;
+    const float hi = zhi + m;
+    // (false for NaN planes; the far margin keeps every pixel's quantised depth below the cleared 2^24 - 1)
+    const bool in_range = zlo - m >= 0.0f && hi < 0.999f;
+    return cover && in_range ? (uint32_t)__builtin_fmaf(hi, 16777215.0f, 2.5f) : 0xffffffffu;
+}
+
+// minimum of v over the wave, wave-uniform (as wave_max_u32)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false));
+    const uint32_t a = __builtin_amdgcn_readlane(v, 15), b = __builtin_amdgcn_readlane(v, 31);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 47), d = __builtin_amdgcn_readlane(v, 63);
+    return min(min(a, b), min(c, d));
+}
 
 template <bool NoDepth, bool Large>
 __device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__restrict__ frame_recs, short2v pix,
@@ -457,8 +516,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
     const Rec *frame_recs = FUSED ? s_recs : recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = FUSED ? s_fd : fdata + (int64_t)b * F;
-    const bool in_frame = i < W && j < H;
-    const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
     if constexpr (FUSED) {
         if (t < F) {
             bool oob;
@@ -644,6 +701,35 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     // the farthest depth the wave's pixels hold; the others can win no pixel.  A segment starts
                     // even (aligned pair reads); the second read of an odd segment's last pair lands on a
                     // valid entry (stale or next) or the sentinel, and an entry run twice changes nothing (min).
+#if DIRT_RASTER_HZ && DIRT_RASTER_OCC
+                    if (!kNoDepth && ns > DIRT_RASTER_OCC_MIN) {
+                        const int bxo = wave_ox(wave), byo = wave_oy(wave);
+                        uint32_t bound = 0xffffffffu;
+                        for (int c0 = 0; c0 < ns; c0 += 64) {
+                            const int kk = c0 + lane;
+                            if (kk < ns)
+                                bound = min(bound, entry_occluder_qmax(t_ent, t_wl[wave][kk], bxo, byo, ti0 + bxo, tj0 + byo));
+                        }
+                        bound = wave_min_u32(bound);
+                        if (bound != 0xffffffffu) {
+                            // in-place compaction to the entries that can still win a pixel (each group's
+                            // offsets are read by every lane before any is written)
+                            int n2 = 0;
+                            for (int c0 = 0; c0 < ns; c0 += 64) {
+                                const int kk = c0 + lane;
+                                const bool tst = kk < ns;
+                                const uint32_t off = tst ? t_wl[wave][kk] : 0u;
+                                const bool live = tst && entry_qmin(t_ent, off, ti0 + bxo, tj0 + byo) <= bound;
+                                const uint64_t lm = __ballot(live);
+                                if (live) t_wl[wave][n2 + lane_rank(lm)] = off;
+                                n2 += __popcll(lm);
+                            }
+                            ns = n2;
+                            if (lane == 0) t_wl[wave][ns] = 256u * sizeof(StripEntry);  // pad / sentinel
+                            wave_lds_sync();
+                        }
+                    }
+#endif
                     int base = 0;
                     int seg = (!kNoDepth && DIRT_RASTER_HZ) ? min(ns, DIRT_RASTER_HZ_MIN) : ns;
                     int rp = seg;  // first list position not yet run or culled
@@ -730,7 +816,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         }
     }
     PHASE_TS(3);
-    if (!in_frame) return;
+    // (the pixel's offset is computed here, after the chunk loop: live across it, it cost a VGPR spill)
+    if (!(i < W && j < H)) return;
+    const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
     float *out = pixels + o * C;
     if (AB & 15) {
         gbuffer[o] = (int32_t)best;

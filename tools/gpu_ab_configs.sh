@@ -7,7 +7,7 @@ mkdir -p $R/gpurun_out
 for rep in $(seq 1 $REPS); do
 for lib in $R/dirt_amd/libdirt_mi355x.so $R/build/variants/*.so; do
   n=$(basename $lib .so)
-  DIRT_MI355X_LIB=$lib timeout -k 10 200 python3 $R/tools/bench_configs.py "$@" > $R/gpurun_out/abc_${n}_$rep.jsonl 2> $R/gpurun_out/abc_${n}_$rep.err
+  DIRT_NO_CPU=1 DIRT_MI355X_LIB=$lib timeout -k 10 300 python3 $R/tools/bench_configs.py "$@" > $R/gpurun_out/abc_${n}_$rep.jsonl 2> $R/gpurun_out/abc_${n}_$rep.err
   rc=$?; [ $rc -ne 0 ] && { echo "$n rc=$rc"; tail -3 $R/gpurun_out/abc_${n}_$rep.err; exit $rc; }
   python3 -c "
 import json,sys
