@@ -319,6 +319,35 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return min(min(a, b), min(c, d));
 }
 
+// The occluder pass over one wave's entry list (out of line: it runs only for long lists, and inlined its
+// registers cost the common path a spill): the block's depth bound from its full-block occluders, then an
+// in-place compaction to the entries whose depth lower bound does not exceed it.  Returns the new length.
+__device__ __noinline__ int occluder_cull(const StripEntry *ent, uint32_t *wl, int ns, int bxo, int byo, int ti0, int tj0)
+{
+    const int lane = threadIdx.x & 63;
+    uint32_t bound = 0xffffffffu;
+    for (int c0 = 0; c0 < ns; c0 += 64) {
+        const int kk = c0 + lane;
+        if (kk < ns) bound = min(bound, entry_occluder_qmax(ent, wl[kk], bxo, byo, ti0 + bxo, tj0 + byo));
+    }
+    bound = wave_min_u32(bound);
+    if (bound == 0xffffffffu) return ns;
+    // (each group's offsets are read by every lane before any is written)
+    int n2 = 0;
+    for (int c0 = 0; c0 < ns; c0 += 64) {
+        const int kk = c0 + lane;
+        const bool tst = kk < ns;
+        const uint32_t off = tst ? wl[kk] : 0u;
+        const bool live = tst && entry_qmin(ent, off, ti0 + bxo, tj0 + byo) <= bound;
+        const uint64_t lm = __ballot(live);
+        if (live) wl[n2 + lane_rank(lm)] = off;
+        n2 += __popcll(lm);
+    }
+    if (lane == 0) wl[n2] = 256u * sizeof(StripEntry);  // pad / sentinel
+    wave_lds_sync();
+    return n2;
+}
+
 template <bool NoDepth, bool Large>
 __device__ __forceinline__ void raster_entry(const EntryRegs &q, const Rec *__restrict__ frame_recs, short2v pix,
                                              float2v pxy, int i, int j, uint64_t &best)
@@ -702,33 +731,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     // even (aligned pair reads); the second read of an odd segment's last pair lands on a
                     // valid entry (stale or next) or the sentinel, and an entry run twice changes nothing (min).
 #if DIRT_RASTER_HZ && DIRT_RASTER_OCC
-                    if (!kNoDepth && ns > DIRT_RASTER_OCC_MIN) {
-                        const int bxo = wave_ox(wave), byo = wave_oy(wave);
-                        uint32_t bound = 0xffffffffu;
-                        for (int c0 = 0; c0 < ns; c0 += 64) {
-                            const int kk = c0 + lane;
-                            if (kk < ns)
-                                bound = min(bound, entry_occluder_qmax(t_ent, t_wl[wave][kk], bxo, byo, ti0 + bxo, tj0 + byo));
-                        }
-                        bound = wave_min_u32(bound);
-                        if (bound != 0xffffffffu) {
-                            // in-place compaction to the entries that can still win a pixel (each group's
-                            // offsets are read by every lane before any is written)
-                            int n2 = 0;
-                            for (int c0 = 0; c0 < ns; c0 += 64) {
-                                const int kk = c0 + lane;
-                                const bool tst = kk < ns;
-                                const uint32_t off = tst ? t_wl[wave][kk] : 0u;
-                                const bool live = tst && entry_qmin(t_ent, off, ti0 + bxo, tj0 + byo) <= bound;
-                                const uint64_t lm = __ballot(live);
-                                if (live) t_wl[wave][n2 + lane_rank(lm)] = off;
-                                n2 += __popcll(lm);
-                            }
-                            ns = n2;
-                            if (lane == 0) t_wl[wave][ns] = 256u * sizeof(StripEntry);  // pad / sentinel
-                            wave_lds_sync();
-                        }
-                    }
+                    if (!kNoDepth && ns > DIRT_RASTER_OCC_MIN)
+                        ns = occluder_cull(t_ent, t_wl[wave], ns, wave_ox(wave), wave_oy(wave), ti0, tj0);
 #endif
                     int base = 0;
                     int seg = (!kNoDepth && DIRT_RASTER_HZ) ? min(ns, DIRT_RASTER_HZ_MIN) : ns;

@@ -87,13 +87,16 @@ def specular_directional(vertex_positions, vertex_normals, vertex_reflectivities
     as_t = lambda x: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
     vertex_normals, vertex_reflectivities = as_t(vertex_normals), as_t(vertex_reflectivities)
     light_direction, light_color = as_t(light_direction), as_t(light_color)
-    camera_position, shininess = as_t(camera_position), as_t(shininess)
+    camera_position = as_t(camera_position)
+    # a Python-number exponent stays a number: no host-to-device copy per call (and the call can be captured
+    # into a HIP graph, where such a copy is not permitted)
+    shininess = shininess if isinstance(shininess, (int, float)) else as_t(shininess)[..., None, None]
     to_light = -light_direction
     reflected = -to_light + 2. * torch.matmul(vertex_normals, to_light[..., :, None]) * vertex_normals
     to_camera = camera_position[..., None, :] - vertex_positions
     cosines = ((to_camera / torch.linalg.norm(to_camera, dim=-1, keepdim=True) + 1.e-12) * reflected).sum(-1, keepdim=True)
     cosines = cosines.abs() if double_sided else cosines.clamp_min(0.)
-    return light_color[..., None, :] * vertex_reflectivities * torch.pow(cosines, shininess[..., None, None])
+    return light_color[..., None, :] * vertex_reflectivities * torch.pow(cosines, shininess)
 
 
 def diffuse_point(vertex_positions, vertex_normals, vertex_colors, light_position, light_color, double_sided=True,
