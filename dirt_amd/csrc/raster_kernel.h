@@ -732,7 +732,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     // valid entry (stale or next) or the sentinel, and an entry run twice changes nothing (min).
 #if DIRT_RASTER_HZ && DIRT_RASTER_OCC
                     if (!kNoDepth && ns > DIRT_RASTER_OCC_MIN)
-                        ns = occluder_cull(t_ent, t_wl[wave], ns, wave_ox(wave), wave_oy(wave), ti0, tj0);
+                        // (readfirstlane: the call returns in a VGPR, and a divergent-looking ns would turn the
+                        // list walks' uniform loop control into exec-masked vector code)
+                        ns = __builtin_amdgcn_readfirstlane(
+                            occluder_cull(t_ent, t_wl[wave], ns, wave_ox(wave), wave_oy(wave), ti0, tj0));
 #endif
                     int base = 0;
                     int seg = (!kNoDepth && DIRT_RASTER_HZ) ? min(ns, DIRT_RASTER_HZ_MIN) : ns;
