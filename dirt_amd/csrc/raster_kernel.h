@@ -329,6 +329,9 @@ __device__ __noinline__ int occluder_cull(const StripEntry *ent, uint32_t *wl, i
     for (int c0 = 0; c0 < ns; c0 += 64) {
         const int kk = c0 + lane;
         if (kk < ns) bound = min(bound, entry_occluder_qmax(ent, wl[kk], bxo, byo, ti0 + bxo, tj0 + byo));
+        // no occluder among the first 64 entries (small triangles, however deep): give up early -- the
+        // pass is an optional cull, and lists of small faces rarely hold one further on
+        if (c0 == 0 && __builtin_amdgcn_ballot_w64(bound != 0xffffffffu) == 0) return ns;
     }
     bound = wave_min_u32(bound);
     if (bound == 0xffffffffu) return ns;
