@@ -246,6 +246,36 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
     }
 };
 
+// dtype / device / layout of an op input as the kernels take it (recorded by autograd, outside the op's node)
+at::Tensor prep(const at::Tensor &x, at::ScalarType t, const at::Device &dev)
+{
+    at::Tensor y = (x.device() != dev || x.scalar_type() != t) ? x.to(dev, t) : x;
+    return y.is_contiguous() ? y : y.contiguous();
+}
+
+// The reference op's shape checks (csrc/rasterise_egl.cpp:310-336, messages as dirt_amd.rasterise_ops._check_shapes)
+void check_shapes(const at::Tensor &bg, const at::Tensor &v, const at::Tensor &vc, const at::Tensor &f, int64_t H,
+                  int64_t W, int64_t C)
+{
+    if (bg.dim() != 4 || bg.size(1) != H || bg.size(2) != W || bg.size(3) != C)
+        throw std::invalid_argument("Rasterise expects background_tensor to be 4D, and bgcolor.shape == [None, height, width, channels]");
+    if (v.dim() != 3 || v.size(2) != 4)
+        throw std::invalid_argument("Rasterise expects vertices to be 3D, and vertices.shape[2] == 4");
+    if (vc.dim() != 3 || vc.size(1) != v.size(1) || vc.size(2) != C)
+        throw std::invalid_argument("Rasterise expects vertex_colors to be 3D, and vertex_colors.shape == [None, vertices.shape[1], channels]");
+    if (f.dim() != 3 || f.size(2) != 3)
+        throw std::invalid_argument("Rasterise expects faces to be 3D, and faces.shape[2] == 3");
+    if (bg.size(0) != v.size(0) || vc.size(0) != v.size(0) || f.size(0) != v.size(0))
+        throw std::invalid_argument("Rasterise expects all arguments to have same leading (batch) dimension");
+    if (C < 1 || C > DIRT_MAX_CHANNELS) throw std::invalid_argument("Rasterise expects 1 <= channels <= 8");
+}
+
+// The public op's fast path (dirt_amd.rasterise_ops._rasterise_batched with tensor inputs): the Python
+// wrapper's conversions and checks done here, in one call.
+variable_list rasterise_checked(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
+                                int64_t H, int64_t W, int64_t C, int64_t bin_capacity, bool want_gbuf,
+                                bool check_faces);
+
 variable_list rasterise(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
                         c10::optional<at::Tensor> camera_pos, int64_t H, int64_t W, int64_t C, int64_t shader_id,
                         int64_t bin_capacity, bool want_gbuf, bool check_faces)
@@ -257,6 +287,29 @@ variable_list rasterise(at::Tensor background, at::Tensor vertices, at::Tensor v
                               want_gbuf, check_faces, grad_possible);
 }
 
+variable_list rasterise_checked(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
+                                int64_t H, int64_t W, int64_t C, int64_t bin_capacity, bool want_gbuf,
+                                bool check_faces)
+{
+    // the tensors' device: the first one on the GPU, else the current HIP device (the Python wrapper's _device_of)
+    const at::Tensor *on_gpu = nullptr;
+    for (const at::Tensor *x : {&background, &vertices, &vertex_colors, &faces})
+        if (x->is_cuda()) {
+            on_gpu = x;
+            break;
+        }
+    if (!on_gpu && c10::hip::device_count() == 0)
+        throw std::runtime_error("dirt_amd.rasterise requires a ROCm/HIP GPU: there is no CPU implementation");
+    const at::Device dev = on_gpu ? on_gpu->device() : at::Device(at::kCUDA, c10::hip::current_device());
+    background = prep(background, at::kFloat, dev);
+    vertices = prep(vertices, at::kFloat, dev);
+    vertex_colors = prep(vertex_colors, at::kFloat, dev);
+    faces = prep(faces, at::kInt, dev);
+    check_shapes(background, vertices, vertex_colors, faces, H, W, C);
+    return rasterise(background, vertices, vertex_colors, faces, c10::nullopt, H, W, C, DIRT_SHADER_GOURAUD,
+                     bin_capacity, want_gbuf, check_faces);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
@@ -264,6 +317,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
     m.doc() = "dirt_amd rasterise op: C++ autograd function over the C ABI of libdirt_mi355x.so";
     m.def("init", &init, "dlopen libdirt_mi355x.so and resolve the C ABI");
     m.def("rasterise", &rasterise, "rasterise forward (+ registered backward)");
+    m.def("rasterise_checked", &rasterise_checked,
+          "Gouraud rasterise of tensor inputs with the wrapper's dtype / device / shape handling");
     m.def("scratch_cache_clear", [](bool force) { g_scratch.clear(force); }, py::arg("force") = false);
     m.def("scratch_cache_size", []() { return g_scratch.size(); });
 }

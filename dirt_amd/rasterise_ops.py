@@ -343,6 +343,17 @@ _CHECK_FACES_DEFAULT = os.environ.get("DIRT_CHECK_FACES", "") not in ("", "0")
 
 def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
                        bin_capacity=0, return_gbuffer=False, want_gbuf=False, check_faces=None):
+    if check_faces is None:
+        check_faces = _CHECK_FACES_DEFAULT
+    ext = _torch_ext()
+    if (ext is not None and camera_pos is None and shader_id == _lib.SHADER_GOURAUD and type(background) is torch.Tensor
+            and type(vertices) is torch.Tensor and type(vertex_colors) is torch.Tensor and type(faces) is torch.Tensor):
+        # fast path: dtype / device / contiguity / shape handling in the C++ op (torch_op.cpp rasterise_checked)
+        outs = ext.rasterise_checked(background, vertices, vertex_colors, faces, int(height), int(width),
+                                     int(channels), int(bin_capacity), bool(want_gbuf), bool(check_faces))
+        if want_gbuf:
+            return outs
+        return (outs[0], outs[1]) if return_gbuffer else outs[0]
     dev = _device_of(background, vertices, vertex_colors, faces, camera_pos)
     background = _as_tensor(background, torch.float32, dev).contiguous()
     vertices = _as_tensor(vertices, torch.float32, dev).contiguous()
@@ -350,11 +361,8 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
     faces = _as_tensor(faces, torch.int32, dev).contiguous()
     camera_pos = _camera(camera_pos, shader_id, dev)
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
-    if check_faces is None:
-        check_faces = _CHECK_FACES_DEFAULT
     args = (background, vertices, vertex_colors, faces, camera_pos, int(height), int(width), int(channels), shader_id,
             int(bin_capacity), bool(want_gbuf), bool(check_faces))
-    ext = _torch_ext()
     outs = ext.rasterise(*args) if ext is not None else _RasteriseFunction.apply(*args)
     if want_gbuf:
         return outs

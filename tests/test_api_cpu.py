@@ -126,3 +126,15 @@ def test_upstream_positional_call_form():
         with pytest.raises(RuntimeError, match="GPU"):
             dirt_amd.rasterise_batch(bg, np.zeros((1, 3, 4), np.float32), np.zeros((1, 3, 3), np.float32),
                                      np.zeros((1, 1, 3), np.int32), 8, 8, 3)
+
+
+def test_tensor_inputs_without_a_gpu_raise_the_same_error():
+    """The C++ fast path of the public op (torch tensors in, torch_op.cpp rasterise_checked) fails like the
+    Python path when there is no HIP device: no CPU fallback."""
+    import torch
+    import dirt_amd
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    t = [torch.zeros((1, 8, 8, 3)), torch.zeros((1, 3, 4)), torch.zeros((1, 3, 3)), torch.zeros((1, 1, 3), dtype=torch.int32)]
+    with pytest.raises(RuntimeError, match="GPU"):
+        dirt_amd.rasterise_batch(*t)
