@@ -68,6 +68,13 @@ inline TileGrid tile_grid(int ntx) { return TileGrid{ntx, (uint32_t)(((1ull << 3
 #ifndef DIRT_RASTER_HZ_MIN
 #define DIRT_RASTER_HZ_MIN 32
 #endif
+// Lists of at least DIRT_RASTER_HZ_DEEP_N entries run only their first DIRT_RASTER_HZ_DEEP before culling.
+#ifndef DIRT_RASTER_HZ_DEEP_N
+#define DIRT_RASTER_HZ_DEEP_N 1000000
+#endif
+#ifndef DIRT_RASTER_HZ_DEEP
+#define DIRT_RASTER_HZ_DEEP 8
+#endif
 // Occluder culling before the entry loop (depth-tested programs): a wave whose list holds more than
 // DIRT_RASTER_OCC_MIN entries first bounds its block's final depth by the nearest entry that covers the whole
 // block (entry_occluder_qmax), then drops every entry whose depth lower bound exceeds it -- in deep scenes
@@ -741,7 +748,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                             occluder_cull(t_ent, t_wl[wave], ns, wave_ox(wave), wave_oy(wave), ti0, tj0));
 #endif
                     int base = 0;
-                    int seg = (!kNoDepth && DIRT_RASTER_HZ) ? min(ns, DIRT_RASTER_HZ_MIN) : ns;
+                    // (a long list -- large overlapping faces -- runs only DIRT_RASTER_HZ_DEEP entries before its
+                    // first cull: they cover the block, and the cull drops most of the rest)
+                    int seg = (!kNoDepth && DIRT_RASTER_HZ)
+                                  ? min(ns, ns >= DIRT_RASTER_HZ_DEEP_N ? DIRT_RASTER_HZ_DEEP : DIRT_RASTER_HZ_MIN)
+                                  : ns;
                     int rp = seg;  // first list position not yet run or culled
                     for (;;) {
                         u32x2 oo = *(lds_u32x2 *)&t_wl[wave][base];
