@@ -228,6 +228,34 @@ __device__ __forceinline__ float pair_scalar(const int32_t *s_gb, const float *s
     return (g1 != -2 && g2 != -2) ? -0.5f * a : 0.0f;
 }
 
+// pair_scalar with pixel p's operands in registers (its g-buffer word, G and I): s = -0.5 sum_c (G(p)+G(q))
+// (I(q)-I(p)), the same operand order as pair_scalar; 0 when either pixel is outside the frame
+template <int CP, int CM>
+__device__ __forceinline__ float pair_scalar_own(int32_t g1, const float *Gp, const float *Ip, const int32_t *s_gb,
+                                                 const float *s_G, const float *s_I, int k2, int C)
+{
+    const int32_t g2 = s_gb[k2];
+    float Gq[CP > CM ? CP : CM], Iq[CP > CM ? CP : CM];
+    if constexpr (CP == 8) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            *reinterpret_cast<float4 *>(&Gq[4 * h]) = *reinterpret_cast<const float4 *>(&s_G[k2 * 8 + 4 * h]);
+            *reinterpret_cast<float4 *>(&Iq[4 * h]) = *reinterpret_cast<const float4 *>(&s_I[k2 * 8 + 4 * h]);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+            Gq[c] = c < C ? s_G[k2 * CP + c] : 0.0f;
+            Iq[c] = c < C ? s_I[k2 * CP + c] : 0.0f;
+        }
+    }
+    float a = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+        if (c < C) a += (Gp[c] + Gq[c]) * (Iq[c] - Ip[c]);
+    return (g1 != -2 && g2 != -2) ? -0.5f * a : 0.0f;
+}
+
 // Index (0..15) of the first lane of this lane's run of equal `key` in its 16-lane DPP row.
 __device__ __forceinline__ int run_start(int key, int lx)  // lx: lane index within its 16-lane DPP row
 {
@@ -319,6 +347,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
     }
     if (t == 0) T.n = 0;
     const int hi0 = tx * TWX - 1, hj0 = ty * kGradTileH - 1;
+    // the staged pixels' g-buffer words and G / I (for the staged pair scalars below, !kRecompute)
+    int32_t gbv[2];
+    float Gv[2][CM], Iv[2][CM];
     {
         // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * NT)
         static_assert(kHaloPix <= 2 * NT, "two staging passes");
@@ -327,9 +358,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
         const int32_t *gb_f = gbuffer + fpix;
         const uint8_t *cov_f = covbits + fpix;
         const float *gp_f = grad_pixels + fpix * C, *px_f = pixels + fpix * C;
-        int32_t gbv[2];
         uint32_t cvv[2];
-        float Gv[2][CM], Iv[2][CM];
         bool ok[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -449,19 +478,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
         // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
         // bottom row of the halo (their one pair into the tile); nothing reads the others
         if constexpr (!kRecompute) {
-        s_sx[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + 1, C);
-        s_sy[kme] = pair_scalar<CP, CM>(s_gb, s_G, s_I, kme, kme + kHalo, C);
-        if (t >= NT - 64 && t - (NT - 64) < 16 + TWX) {
-            // the 16 + TWX halo pairs into the tile, one per lane of the last wave and one pair_scalar for
-            // all of them (the LDS reads of a pair are wide: spreading them over every wave, or a branch per
-            // axis, would cost each wave two more rounds of them)
-            const int h = t - (NT - 64);
-            const bool xa = h < 16;
-            const int k = xa ? (h + 1) * kHalo : h - 15;  // (0, h + 1) or (h - 15, 0)
-            const float sv = pair_scalar<CP, CM>(s_gb, s_G, s_I, k, k + (xa ? 1 : kHalo), C);
-            if (xa) s_sx[k] = sv;
-            else s_sy[k] = sv;
-        }
+            // staged pair scalars: the lane that staged region pixel k computes the pairs starting there that
+            // phase B reads -- (k, k+x) for hx in 0..TWX, hy in 1..16 and (k, k+y) for hx in 1..TWX, hy in 0..16
+            // -- with k's own G / I still in its registers (only the neighbour's come from LDS)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int k = t + NT * u;
+                if (k >= kHaloPix) continue;
+                const int hx = k % kHalo, hy = k / kHalo;
+                const bool need_x = hx <= TWX && hy >= 1 && hy <= kGradTileH;
+                const bool need_y = hx >= 1 && hx <= TWX && hy <= kGradTileH;
+                if (need_x) s_sx[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + 1, C);
+                if (need_y) s_sy[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + kHalo, C);
+            }
         }
         if (filler) {
             bool small = true;
