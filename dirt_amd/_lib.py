@@ -30,6 +30,7 @@ MAX_DIM = 8192
 ABI_VERSION = 8
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
+FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes
 BWD_ACCUMULATE = 1     # dirt_rasterise_bwd / dirt_rasterise_bwd_recompute flags
 BWD_SCRATCH_CLEAN = 2  # dirt_rasterise_bwd_recompute: the workspace's bin counters are clean
 

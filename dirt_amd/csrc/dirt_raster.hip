@@ -309,6 +309,8 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
     // small frames (Gouraud, F <= kFusedMaxF): the raster sets up the faces itself (one launch, no bins)
     const bool fused = shader_id == DIRT_SHADER_GOURAUD && F > 0 && F <= kFusedMaxF;
+    // occluder culling of long per-wave entry lists (deep scenes), opt-in (raster_kernel.h, OCC)
+    const bool deep = (flags & DIRT_FWD_DEEP_CULL) != 0 && shader_id == DIRT_SHADER_GOURAUD && !nopix;
     if (F > 0 && !fused) {
         ProfScope ps(K_SETUP, stream);
         launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream, zero_grad_vertices,
@@ -346,6 +348,12 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
             L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
             zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
             zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo);          \
+    else if (deep && !fused && !want_gb)                                                                         \
+        raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, false, false, false, true><<<grid, dim3(256), 0, stream>>>(     \
+            background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
+            L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
+            zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb);               \
     else if (fused && want_gb)                                                                                   \
         raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, true, true><<<grid, dim3(256), 0, stream>>>(                   \
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \

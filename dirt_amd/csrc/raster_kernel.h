@@ -75,13 +75,12 @@ inline TileGrid tile_grid(int ntx) { return TileGrid{ntx, (uint32_t)(((1ull << 3
 #ifndef DIRT_RASTER_HZ_DEEP
 #define DIRT_RASTER_HZ_DEEP 8
 #endif
-// Occluder culling before the entry loop (depth-tested programs): a wave whose list holds more than
-// DIRT_RASTER_OCC_MIN entries first bounds its block's final depth by the nearest entry that covers the whole
-// block (entry_occluder_qmax), then drops every entry whose depth lower bound exceeds it -- in deep scenes
-// (large overlapping triangles) most of the list, before any of it runs.  Results are bit-identical.
-#ifndef DIRT_RASTER_OCC
-#define DIRT_RASTER_OCC 1
-#endif
+// Occluder culling before the entry loop (the OCC instantiation, dirt_rasterise_fwd flag DIRT_FWD_DEEP_CULL): a
+// wave whose list holds more than DIRT_RASTER_OCC_MIN entries first bounds its block's final depth by the
+// nearest entry that covers the whole block (entry_occluder_qmax), then drops every entry whose depth lower
+// bound exceeds it -- in deep scenes (large overlapping triangles) most of the list, before any of it runs.
+// Results are bit-identical.  Opt-in: the pass runs only for long lists, but its mere presence costs the
+// common case (c3) ~0.6 us of raster time (profiles/r04/ab_occluder), while deep scenes gain 15 %.
 #ifndef DIRT_RASTER_OCC_MIN
 #define DIRT_RASTER_OCC_MIN 32
 #endif
@@ -497,7 +496,8 @@ constexpr int kFusedMaxF = 32;
 
 // NOPIX (Gouraud): coverage-only resolve for dirt_rasterise_bwd_recompute -- the g-buffer and the
 // neighbour-coverage bits the backward reads, no pixels (no background or colour loads, no pixel stores).
-template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false, bool NOPIX = false>
+template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false, bool NOPIX = false,
+          bool OCC = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
@@ -740,8 +740,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     // the farthest depth the wave's pixels hold; the others can win no pixel.  A segment starts
                     // even (aligned pair reads); the second read of an odd segment's last pair lands on a
                     // valid entry (stale or next) or the sentinel, and an entry run twice changes nothing (min).
-#if DIRT_RASTER_HZ && DIRT_RASTER_OCC
-                    if (!kNoDepth && ns > DIRT_RASTER_OCC_MIN)
+#if DIRT_RASTER_HZ
+                    if (OCC && !kNoDepth && ns > DIRT_RASTER_OCC_MIN)
                         // (readfirstlane: the call returns in a VGPR, and a divergent-looking ns would turn the
                         // list walks' uniform loop control into exec-masked vector code)
                         ns = __builtin_amdgcn_readfirstlane(

@@ -134,7 +134,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
     static variable_list forward(AutogradContext *ctx, at::Tensor background, at::Tensor vertices,
                                  at::Tensor vertex_colors, at::Tensor faces, c10::optional<at::Tensor> camera_pos,
                                  int64_t H, int64_t W, int64_t C, int64_t shader_id, int64_t bin_capacity,
-                                 bool want_gbuf, bool check_faces, bool grad_possible)
+                                 bool want_gbuf, bool check_faces, bool grad_possible, int64_t fwd_flags)
     {
         const int64_t B = vertices.size(0), V = vertices.size(1), F = faces.size(1);
         const at::Device dev = vertices.device();
@@ -181,7 +181,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
                                     vertex_colors.data_ptr<float>(), faces.data_ptr<int32_t>(), (int)B, (int)H, (int)W,
                                     (int)C, (int)V, (int)F, pixels.data_ptr<float>(), gbuffer.data_ptr<int32_t>(),
                                     saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
-                                    DIRT_FWD_SCRATCH_CLEAN, zgv, zgc, depth.data_ptr<float>(), bary.data_ptr<float>(),
+                                    (unsigned)fwd_flags | DIRT_FWD_SCRATCH_CLEAN, zgv, zgc, depth.data_ptr<float>(), bary.data_ptr<float>(),
                                     face.data_ptr<int32_t>(), stream));
             out.push_back(depth);
             out.push_back(bary);
@@ -191,8 +191,8 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
             check(g_api.fwd(background.data_ptr<float>(), vertices.data_ptr<float>(), vertex_colors.data_ptr<float>(),
                             faces.data_ptr<int32_t>(), cam, (int)B, (int)H, (int)W, (int)C, (int)V, (int)F,
                             (int)shader_id, pixels.data_ptr<float>(), gbuffer.data_ptr<int32_t>(), saved.data_ptr(),
-                            saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity, DIRT_FWD_SCRATCH_CLEAN, zgv,
-                            zgc, stream));
+                            saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
+                            (unsigned)fwd_flags | DIRT_FWD_SCRATCH_CLEAN, zgv, zgc, stream));
         }
         drop.armed = false;
         ctx->save_for_backward({vertices, vertex_colors, faces, pixels, gbuffer, saved});
@@ -242,7 +242,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
                         (int)B, (int)H, (int)W, (int)C, (int)V, (int)F, gv.data_ptr<float>(), gc.data_ptr<float>(),
                         gbg.data_ptr<float>(), flags, stream));
         return {gbg, gv, gc, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
-                at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
+                at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
     }
 };
 
@@ -274,22 +274,22 @@ void check_shapes(const at::Tensor &bg, const at::Tensor &v, const at::Tensor &v
 // wrapper's conversions and checks done here, in one call.
 variable_list rasterise_checked(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
                                 int64_t H, int64_t W, int64_t C, int64_t bin_capacity, bool want_gbuf,
-                                bool check_faces);
+                                bool check_faces, int64_t fwd_flags);
 
 variable_list rasterise(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
                         c10::optional<at::Tensor> camera_pos, int64_t H, int64_t W, int64_t C, int64_t shader_id,
-                        int64_t bin_capacity, bool want_gbuf, bool check_faces)
+                        int64_t bin_capacity, bool want_gbuf, bool check_faces, int64_t fwd_flags)
 {
     if (!g_api.fwd) throw std::runtime_error("_dirt_torch.init(path) was not called");
     const bool grad_possible = at::GradMode::is_enabled() &&
                                (background.requires_grad() || vertices.requires_grad() || vertex_colors.requires_grad());
     return RasteriseFn::apply(background, vertices, vertex_colors, faces, camera_pos, H, W, C, shader_id, bin_capacity,
-                              want_gbuf, check_faces, grad_possible);
+                              want_gbuf, check_faces, grad_possible, fwd_flags);
 }
 
 variable_list rasterise_checked(at::Tensor background, at::Tensor vertices, at::Tensor vertex_colors, at::Tensor faces,
                                 int64_t H, int64_t W, int64_t C, int64_t bin_capacity, bool want_gbuf,
-                                bool check_faces)
+                                bool check_faces, int64_t fwd_flags)
 {
     // the tensors' device: the first one on the GPU, else the current HIP device (the Python wrapper's _device_of)
     const at::Tensor *on_gpu = nullptr;
@@ -307,7 +307,7 @@ variable_list rasterise_checked(at::Tensor background, at::Tensor vertices, at::
     faces = prep(faces, at::kInt, dev);
     check_shapes(background, vertices, vertex_colors, faces, H, W, C);
     return rasterise(background, vertices, vertex_colors, faces, c10::nullopt, H, W, C, DIRT_SHADER_GOURAUD,
-                     bin_capacity, want_gbuf, check_faces);
+                     bin_capacity, want_gbuf, check_faces, fwd_flags);
 }
 
 }  // namespace
@@ -316,9 +316,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
 {
     m.doc() = "dirt_amd rasterise op: C++ autograd function over the C ABI of libdirt_mi355x.so";
     m.def("init", &init, "dlopen libdirt_mi355x.so and resolve the C ABI");
-    m.def("rasterise", &rasterise, "rasterise forward (+ registered backward)");
+    m.def("rasterise", &rasterise, "rasterise forward (+ registered backward)", py::arg("background"),
+          py::arg("vertices"), py::arg("vertex_colors"), py::arg("faces"), py::arg("camera_pos"), py::arg("height"),
+          py::arg("width"), py::arg("channels"), py::arg("shader_id"), py::arg("bin_capacity"), py::arg("want_gbuf"),
+          py::arg("check_faces"), py::arg("fwd_flags") = (int64_t)DIRT_FWD_SCRATCH_CLEAN);
     m.def("rasterise_checked", &rasterise_checked,
-          "Gouraud rasterise of tensor inputs with the wrapper's dtype / device / shape handling");
+          "Gouraud rasterise of tensor inputs with the wrapper's dtype / device / shape handling",
+          py::arg("background"), py::arg("vertices"), py::arg("vertex_colors"), py::arg("faces"), py::arg("height"),
+          py::arg("width"), py::arg("channels"), py::arg("bin_capacity"), py::arg("want_gbuf"), py::arg("check_faces"),
+          py::arg("fwd_flags") = (int64_t)DIRT_FWD_SCRATCH_CLEAN);
     m.def("scratch_cache_clear", [](bool force) { g_scratch.clear(force); }, py::arg("force") = false);
     m.def("scratch_cache_size", []() { return g_scratch.size(); });
 }

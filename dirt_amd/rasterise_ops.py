@@ -198,7 +198,7 @@ class _RasteriseFunction(torch.autograd.Function):
                 background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
                 B, H, W, C, V, F, shader_id, pixels.data_ptr(), gbuffer.data_ptr(),
                 saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, bin_capacity,
-                _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1], stream))
+                _FWD_FLAGS, zg[0], zg[1], stream))
             return ()
         dev = vertices.device
         depth = torch.empty((B, H, W), dtype=torch.float32, device=dev)
@@ -207,7 +207,7 @@ class _RasteriseFunction(torch.autograd.Function):
         _lib.check(lib.dirt_rasterise_fwd_gbuffer(
             background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
             B, H, W, C, V, F, pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(), saved_bytes,
-            scratch.data_ptr(), scratch_bytes, bin_capacity, _lib.FWD_SCRATCH_CLEAN, zg[0], zg[1],
+            scratch.data_ptr(), scratch_bytes, bin_capacity, _FWD_FLAGS, zg[0], zg[1],
             depth.data_ptr(), bary.data_ptr(), face_ids.data_ptr(), stream))
         return (depth, bary, face_ids)
 
@@ -339,6 +339,10 @@ def workspace_cache_size():
 
 # DIRT_CHECK_FACES=1: every call range-checks its face indices (one kernel + a host sync; off by default)
 _CHECK_FACES_DEFAULT = os.environ.get("DIRT_CHECK_FACES", "") not in ("", "0")
+# DIRT_DEEP_CULL=1: Gouraud forwards cull occluded triangles of long per-tile lists (DIRT_FWD_DEEP_CULL): for deep
+# scenes of large overlapping triangles; identical results, scenes of small triangles run slightly faster without
+_FWD_FLAGS = _lib.FWD_SCRATCH_CLEAN | (_lib.FWD_DEEP_CULL if os.environ.get("DIRT_DEEP_CULL", "") not in ("", "0")
+                                       else 0)
 
 
 def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,
@@ -350,7 +354,7 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
             and type(vertices) is torch.Tensor and type(vertex_colors) is torch.Tensor and type(faces) is torch.Tensor):
         # fast path: dtype / device / contiguity / shape handling in the C++ op (torch_op.cpp rasterise_checked)
         outs = ext.rasterise_checked(background, vertices, vertex_colors, faces, int(height), int(width),
-                                     int(channels), int(bin_capacity), bool(want_gbuf), bool(check_faces))
+                                     int(channels), int(bin_capacity), bool(want_gbuf), bool(check_faces), _FWD_FLAGS)
         if want_gbuf:
             return outs
         return (outs[0], outs[1]) if return_gbuffer else outs[0]
@@ -363,7 +367,7 @@ def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, h
     _check_shapes(background, vertices, vertex_colors, faces, height, width, channels)
     args = (background, vertices, vertex_colors, faces, camera_pos, int(height), int(width), int(channels), shader_id,
             int(bin_capacity), bool(want_gbuf), bool(check_faces))
-    outs = ext.rasterise(*args) if ext is not None else _RasteriseFunction.apply(*args)
+    outs = ext.rasterise(*args, _FWD_FLAGS) if ext is not None else _RasteriseFunction.apply(*args)
     if want_gbuf:
         return outs
     pixels, gbuffer = outs

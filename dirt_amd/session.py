@@ -24,8 +24,10 @@ from . import _lib
 
 
 class RasteriseSession:
-    def __init__(self, B, H, W, C, V, F, device=None, bin_capacity=0, shader_id=_lib.SHADER_GOURAUD):
+    def __init__(self, B, H, W, C, V, F, device=None, bin_capacity=0, shader_id=_lib.SHADER_GOURAUD, deep_cull=False):
+        """deep_cull: occluder culling for deep scenes (DIRT_FWD_DEEP_CULL: large overlapping triangles)."""
         self.dims = (B, H, W, C, V, F)
+        self.fwd_flags = _lib.FWD_SCRATCH_CLEAN | (_lib.FWD_DEEP_CULL if deep_cull else 0)
         self.shader_id = shader_id
         dev = torch.device(device) if device is not None else torch.device("cuda")
         if dev.type == "cuda" and dev.index is None:  # "cuda" means the current device: compare as cuda:N
@@ -96,7 +98,7 @@ class RasteriseSession:
             background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
             B, H, W, C, V, F, self.shader_id, self.pixels.data_ptr(), self.gbuffer.data_ptr(),
             self.saved.data_ptr(), self.saved_bytes, self.scratch.data_ptr(), self.scratch_bytes,
-            self.bin_capacity, _lib.FWD_SCRATCH_CLEAN, self.grad_vertices.data_ptr(),
+            self.bin_capacity, self.fwd_flags, self.grad_vertices.data_ptr(),
             self.grad_vertex_colors.data_ptr(), stream))
         return self.pixels
 

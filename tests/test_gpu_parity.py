@@ -389,6 +389,49 @@ def test_deep_depth_complexity_culling(perspective):
     check_scene(bg, v2, c2, f2)
 
 
+def _deep_scene(perspective, W=96, H=80, F=400, seed=11):
+    bg, v, c, f = scenes.random_triangles(F=F, W=W, H=H, radius_px=70.0, seed=seed, perspective=perspective)
+    dup = f[:120].copy()                                   # identical planes, higher face index
+    near = f[120:200].copy()                               # own vertices, depth nudged by ~1e-7
+    vn = v[near.reshape(-1)].copy()
+    vn[:, 2] += np.float32(1e-7) * vn[:, 3]
+    near = (v.shape[0] + np.arange(near.size, dtype=np.int32)).reshape(-1, 3)
+    cn = c[f[120:200].reshape(-1)]
+    return bg, np.concatenate([v, vn]).astype(np.float32), np.concatenate([c, cn]).astype(np.float32), \
+        np.concatenate([f, dup, near]).astype(np.int32)
+
+
+@pytest.mark.parametrize("scene", ["deep_affine", "deep_perspective", "r64_1024", "c3_seed0"])
+def test_deep_cull_flag_bit_exact(scene):
+    """DIRT_FWD_DEEP_CULL (the raster's occluder pass over long per-wave lists, raster_kernel.h OCC): the same
+    g-buffer, pixels and gradients as the default forward and the oracle -- deep scenes with exact and
+    sub-quantum depth ties, the r = 64 px stress distribution at 1024^2, and config 3 (short lists: the pass
+    rarely runs)."""
+    from dirt_amd.session import RasteriseSession
+    if scene.startswith("deep"):
+        sc = _deep_scene(scene.endswith("perspective"))
+    elif scene == "r64_1024":
+        sc = scenes.random_triangles(F=12000, W=1024, H=1024, radius_px=64.0, seed=7)
+    else:
+        sc = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
+    bg, v, c, f = (a[None] for a in sc)
+    g = np.random.default_rng(3).standard_normal(bg.shape).astype(np.float32)
+    outs = []
+    for deep in (False, True):
+        sess = RasteriseSession(*bg.shape, v.shape[1], f.shape[1], device="cuda", deep_cull=deep)
+        sess.forward(*(_gpu(a) for a in (bg, v, c, f)))
+        gbg, gv, gc = (t.cpu().numpy() for t in sess.backward(_gpu(g)))
+        outs.append((sess.gbuffer.cpu().numpy(), sess.pixels.cpu().numpy(), gbg, gv, gc))
+    px, gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+    rgv, rgc, rgbg = oracle.rasterise_bwd(v, c, f, px, g, gb)
+    for gbuf, pix, gbg, gv, gc in outs:
+        np.testing.assert_array_equal(gbuf, gb)
+        np.testing.assert_array_equal(pix, px)
+        np.testing.assert_array_equal(gbg, rgbg)
+        assert_close_grad(gc, rgc, "grad_vertex_colors")
+        assert_close_grad(gv, rgv, "grad_vertices")
+
+
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUZZ_FIRST", "0")),
                                          int(os.environ.get("DIRT_FUZZ_SEEDS", "36"))))
 def test_fuzz_adversarial_scenes(seed):

@@ -29,6 +29,9 @@ CONFIGS = {
     "c5_batch8x20k_1024x1024x3_per_gpu": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024, seed=b)
                                                   for b in range(8)],
     "c3_stress_r64_1024x1024x3": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, radius_px=64.0, seed=0)],
+    # the same with the forward's occluder culling (DIRT_FWD_DEEP_CULL, RasteriseSession(deep_cull=True))
+    "c3_stress_r64_1024x1024x3_deep_cull": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, radius_px=64.0,
+                                                                            seed=0)],
     # a mesh crowded into the centre 1/16 of each frame at config 5's per-rank batch, at the
     # default bin capacity and with the slabs forced small (1024 entries: the crowded tiles overflow and take
     # the all-records path), to price the overflow path
@@ -146,7 +149,7 @@ def run(name, frames, steps=100):
     V, F = v.shape[1], f.shape[1]
     g = torch.randn((B, H, W, C), device=dev)
     cap = BIN_CAPACITY.get(name, 0)
-    sess = RasteriseSession(B, H, W, C, V, F, device=dev, bin_capacity=cap)
+    sess = RasteriseSession(B, H, W, C, V, F, device=dev, bin_capacity=cap, deep_cull=name.endswith("deep_cull"))
 
     def step():
         sess.forward(bg, v, c, f)
