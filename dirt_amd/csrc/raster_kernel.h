@@ -473,6 +473,12 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const RasterPart &r, cons
 // staging + loop (bin filter only), 4 skip the resolve (g-buffer only), 8 skip the bin filter too,
 // 32 no neighbour-coverage bits, 64 no colour loads (lambda written), 128 phase timestamps, 512 / 1024 / 2048 one
 // extra dependent global round trip before the slab loads / before the colour loads / before the record loads
+// extra kernel attributes for experiments, e.g. -DDIRT_RASTER_ATTR='__attribute__((amdgpu_num_sgpr(80)))': 256-thread
+// workgroups are admitted per CU up to floor(800 / (ceil(sgpr / 16) * 16 + 16)) -- 7 at 82-96 SGPRs, 8 at <= 80
+// (MI355X_MICROARCH.md, residency), whatever the VGPR budget allows
+#ifndef DIRT_RASTER_ATTR
+#define DIRT_RASTER_ATTR
+#endif
 #ifndef DIRT_RASTER_WAVES
 #define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
                              // the procedural programs and the generic-C path keep their natural allocation)
@@ -498,7 +504,7 @@ constexpr int kFusedMaxF = 32;
 // neighbour-coverage bits the backward reads, no pixels (no background or colour loads, no pixel stores).
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false, bool NOPIX = false,
           bool OCC = false>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) DIRT_RASTER_ATTR void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
                                                      const uint2 *__restrict__ bins, uint32_t slab,
@@ -550,7 +556,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int lx = wave_ox(wave) + lane % kWaveW, ly = wave_oy(wave) + lane / kWaveW;
+#ifndef DIRT_RASTER_REMAT_IJ
+#define DIRT_RASTER_REMAT_IJ 0
+#endif
+#if DIRT_RASTER_REMAT_IJ
+    const int i0_ = tx * kTile + lx, j0_ = ty * kTile + ly;  // (the resolve recomputes them)
+#define i i0_
+#define j j0_
+#else
     const int i = tx * kTile + lx, j = ty * kTile + ly;
+#endif
     const int dx = lx * 256, dy = ly * 256;  // offset from the tile origin (sub-pixels)
     const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
     const Rec *frame_recs = FUSED ? s_recs : recs + (int64_t)b * nrec;
@@ -591,9 +606,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     constexpr int U = kFilterBlock / 64;
     uint2 ev[U];
     auto load_chunk = [&](uint32_t chunk) {
+        // (the lane index from an opaque mbcnt: recomputed here instead of kept live across the chunk loop)
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t idx = chunk + wave * kFilterBlock + u * 64 + lane;
+            const uint32_t idx = chunk + wave * kFilterBlock + u * 64 + ln;
             ev[u] = slab_bins[min(idx, slab - 1u)];
         }
     };
@@ -687,7 +705,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             int pre[kStrips + 1];
             pre[0] = 0;
 #pragma unroll
-            for (int w = 0; w < kStrips; ++w) pre[w + 1] = pre[w] + t_nw[par][w];
+            // (wave-uniform: scalar registers, not four VGPRs live through the staging rounds)
+            for (int w = 0; w < kStrips; ++w) pre[w + 1] = pre[w] + __builtin_amdgcn_readfirstlane(t_nw[par][w]);
             const int n_list = pre[kStrips];
             if (AB & 2) {
                 best += (uint64_t)n_list;
@@ -837,6 +856,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         }
     }
     PHASE_TS(3);
+#if DIRT_RASTER_REMAT_IJ
+#undef i
+#undef j
+    // the lane's pixel again, from an opaque copy of threadIdx.x: the compiler cannot reuse the values computed
+    // before the chunk loop, so they need not stay live (in VGPRs) across it
+    int i, j;
+    {
+        int t2 = threadIdx.x;
+        asm volatile("" : "+v"(t2));
+        const int lane2 = t2 & 63, wave2 = __builtin_amdgcn_readfirstlane(t2 >> 6);
+        i = tx * kTile + wave_ox(wave2) + lane2 % kWaveW;
+        j = ty * kTile + wave_oy(wave2) + lane2 / kWaveW;
+    }
+#endif
     // (the pixel's offset is computed here, after the chunk loop: live across it, it cost a VGPR spill)
     if (!(i < W && j < H)) return;
     const int64_t o = ((int64_t)b * H + (H - 1 - j)) * W + i;
