@@ -78,11 +78,13 @@ def unit(v):
     return v / torch.linalg.norm(v)
 
 
-def gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu=False):
+def gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu=False, batched=False):
     """The three G-buffer renders of samples/deferred.py:63-83 ([H,W,3] each) and the clip vertices.
 
     geometry_on_cpu: compute the clip vertices and normals on the CPU (differentiably) and move them to
-    Vw's device, so that two renderers compared on two devices see bit-identical inputs."""
+    Vw's device, so that two renderers compared on two devices see bit-identical inputs.
+    batched: the three renders as one rasterise_batch call of three frames sharing the geometry (the same
+    G-buffers and gradients; one op call instead of three)."""
     dev = Vw.device
     Vx = Vw.cpu() if geometry_on_cpu else Vw
     view, proj = camera(H, W, Vx.device)
@@ -91,6 +93,14 @@ def gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu=False):
     normals = lighting.vertex_normals(Vx, faces.to(Vx.device).long()).to(dev)
     ninf = torch.full((H, W, 3), float("-inf"), device=dev)
     zero = torch.zeros((H, W, 3), device=dev)
+    if batched:
+        import dirt_amd
+        bg = torch.stack([ninf, zero, ninf])
+        cols = torch.stack([Vw.to(dev), albedo.to(dev), normals])
+        f3 = faces.int()[None].expand(3, -1, -1)
+        pos, col, nrm = dirt_amd.rasterise_batch(bg, clip[None].expand(3, -1, -1), cols, f3, height=H, width=W,
+                                                 channels=3).unbind(0)
+        return pos, col, nrm, clip
     pos = render(ninf, clip, Vw, faces, H, W, 3)
     col = render(zero, clip, albedo, faces, H, W, 3)
     nrm = render(ninf, clip, normals, faces, H, W, 3)
@@ -127,8 +137,8 @@ def loss_fn(pixels, valid, weights, mask=None):
     return torch.where(m, pixels * weights, torch.zeros_like(pixels)).sum()
 
 
-def chain(render, Vw, faces, albedo, H, W, weights, mask=None, geometry_on_cpu=False):
-    pos, col, nrm, _ = gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu)
+def chain(render, Vw, faces, albedo, H, W, weights, mask=None, geometry_on_cpu=False, batched=False):
+    pos, col, nrm, _ = gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu, batched)
     pixels, valid = shade(pos, col, nrm, H, W)
     return loss_fn(pixels, valid, weights, mask), pixels, valid
 

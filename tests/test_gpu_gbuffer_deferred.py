@@ -237,3 +237,26 @@ def test_config4_deferred_chain_finite_differences():
     rel = np.abs(num - ana) / scale
     assert np.median(rel) < 0.05 and rel.max() < 0.25, (num, ana)
     assert np.corrcoef(num, ana)[0, 1] > 0.95
+
+
+def test_config4_batched_gbuffer_renders_match_three_calls():
+    """The three G-buffer renders of samples/deferred.py:63-83 as one rasterise_batch call of three frames (the
+    geometry shared, tests/deferred_pipeline.py batched=True): bit-identical G-buffers, the same loss and
+    gradient to the world vertices as the three separate calls."""
+    import deferred_pipeline as dp
+    dev = torch.device("cuda", 0)
+    world, faces, albedo = dp.grid_surface(n=60)
+    H = W = 256
+    wts = torch.rand((H, W, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    res = []
+    for batched in (False, True):
+        Vw = torch.from_numpy(world).to(dev).requires_grad_(True)
+        L, px, valid = dp.chain(dp.hip_render, Vw, torch.from_numpy(faces).to(dev), torch.from_numpy(albedo).to(dev),
+                                H, W, wts, batched=batched)
+        g, = torch.autograd.grad(L, [Vw])
+        res.append((L.detach(), px.detach(), valid, g))
+    (L0, p0, v0, g0), (L1, p1, v1, g1) = res
+    assert torch.equal(v0, v1)
+    assert torch.equal(torch.where(v0, p0, torch.zeros_like(p0)), torch.where(v1, p1, torch.zeros_like(p1)))
+    torch.testing.assert_close(L1, L0, rtol=1e-6, atol=0)
+    torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-5 * float(g0.abs().max()))

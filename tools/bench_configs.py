@@ -76,7 +76,7 @@ def cpu_oracle(host, g, budget_s=3.0):
             "cpu_ms_per_step": round(t * 1e3, 2)}
 
 
-def deferred_chain(steps=20):
+def deferred_chain(steps=20, batched=False):
     """c4 as the reference sample runs it: three 3-channel G-buffer renders + dilation + lighting + loss,
     backward to world-space vertices (tests/deferred_pipeline.py), through dirt_amd.rasterise + autograd.
     Reported eager (host-issued every step), as one captured HIP graph per step (device time: the whole
@@ -92,7 +92,7 @@ def deferred_chain(steps=20):
     out = {}
 
     def step():
-        L, _, _ = dp.chain(dp.hip_render, Vw, f, al, H, W, wts)
+        L, _, _ = dp.chain(dp.hip_render, Vw, f, al, H, W, wts, batched=batched)
         out["g"] = torch.autograd.grad(L, [Vw])[0]
 
     for _ in range(3):
@@ -111,7 +111,8 @@ def deferred_chain(steps=20):
         step()
     t_issue = (time.perf_counter() - t0) / steps
     torch.cuda.synchronize()
-    res = {"config": "c4_deferred_chain_3x512x512x3_grad_to_world_vertices", "faces": len(faces),
+    res = {"config": "c4_deferred_chain_3x512x512x3_grad_to_world_vertices" + ("_batched" if batched else ""),
+           "faces": len(faces),
            "ms_per_step_eager": round(dt * 1e3, 3), "host_issue_ms_per_step": round(t_issue * 1e3, 3),
            "Mpixels_per_s_fwd_bwd": round(H * W / dt / 1e6, 1)}
     try:
@@ -194,6 +195,7 @@ def main():
             print(json.dumps(run(name, make())), flush=True)
     if not sel or any(k in "c4_deferred_chain" for k in sel):
         print(json.dumps(deferred_chain()), flush=True)
+        print(json.dumps(deferred_chain(batched=True)), flush=True)
 
 
 if __name__ == "__main__":
