@@ -307,8 +307,10 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     // count sets and parity words: one memset, unless the caller vouches that the scratch is clean
     // (DIRT_FWD_SCRATCH_CLEAN: zeroed once and since used only by forwards of the same layout)
     if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
-    // small frames (Gouraud, F <= kFusedMaxF): the raster sets up the faces itself (one launch, no bins)
-    const bool fused = shader_id == DIRT_SHADER_GOURAUD && F > 0 && F <= kFusedMaxF;
+    // small scenes (Gouraud, F <= kFusedMaxF, at most kFusedMaxTiles tiles): the raster sets up the faces itself
+    // (one launch, no bins)
+    const bool fused = shader_id == DIRT_SHADER_GOURAUD && F > 0 && F <= kFusedMaxF &&
+                       (int64_t)B * L.ntiles <= kFusedMaxTiles;
     // occluder culling of long per-wave entry lists (deep scenes), opt-in (raster_kernel.h, OCC)
     const bool deep = (flags & DIRT_FWD_DEEP_CULL) != 0 && shader_id == DIRT_SHADER_GOURAUD && !nopix;
     if (F > 0 && !fused) {

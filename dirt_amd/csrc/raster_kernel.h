@@ -499,6 +499,13 @@ struct GbufOut {
 // its tile (the overflow path's all-records filter, reading LDS); the workgroup of tile 0 writes the records
 // and FaceData of its frame to `saved` for the backward.  One launch instead of two for small scenes.
 constexpr int kFusedMaxF = 32;
+// ... and of at most kFusedMaxTiles tiles in the batch: every workgroup repeats the frame's setup
+// (~1 us of dependent latency at the start of its life), which a large frame's many rounds of workgroups would
+// pay again and again -- past a few rounds the separate setup launch (~5 us) and the bins are cheaper
+#ifndef DIRT_FUSED_MAX_TILES
+#define DIRT_FUSED_MAX_TILES 8192
+#endif
+constexpr int64_t kFusedMaxTiles = DIRT_FUSED_MAX_TILES;
 
 // NOPIX (Gouraud): coverage-only resolve for dirt_rasterise_bwd_recompute -- the g-buffer and the
 // neighbour-coverage bits the backward reads, no pixels (no background or colour loads, no pixel stores).

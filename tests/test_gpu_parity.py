@@ -659,6 +659,12 @@ def test_fused_small_scene_forward(seed):
     check_scene(*scene, seed=seed)
 
 
+def test_few_faces_on_a_large_frame_take_the_binned_path():
+    """12 faces on a 2048^2 frame (16384 tiles, past kFusedMaxTiles): the setup launch + bins instead of the
+    fused forward; bit-exact as everywhere."""
+    check_scene(*scenes.cube_scene(W=2048, H=2048), strict=True)
+
+
 def test_fused_small_scene_clipping_and_shared_mesh():
     bg, v, c, f = scenes.clipping_scene()
     check_scene(bg, v, c, f[:32])

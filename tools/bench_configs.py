@@ -24,6 +24,9 @@ from dirt_amd.session import RasteriseSession  # noqa: E402
 CONFIGS = {
     "c1_readme_square_128x128x1": lambda: [scenes.readme_square()],
     "c2_cube_256x256x3": lambda: [scenes.cube_scene()],
+    # the cube at 4096^2: 12 faces over 65536 tiles (past kFusedMaxTiles: setup launch + bins, not the fused
+    # forward -- ADVICE r3's large-frame case)
+    "c2_cube_4096x4096x3": lambda: [scenes.cube_scene(W=4096, H=4096)],
     "c3_random50k_1024x1024x3": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)],
     "c4_deferred20k_512x512x7": lambda: [scenes.deferred_mesh_scene()],
     "c5_batch8x20k_1024x1024x3_per_gpu": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024, seed=b)
