@@ -477,11 +477,13 @@ __device__ __forceinline__ uint32_t neighbour_coverage(const RasterPart &r, cons
 // workgroups are admitted per CU up to floor(800 / (ceil(sgpr / 16) * 16 + 16)) -- 7 at 82-96 SGPRs, 8 at <= 80
 // (MI355X_MICROARCH.md, residency), whatever the VGPR budget allows
 #ifndef DIRT_RASTER_ATTR
-#define DIRT_RASTER_ATTR
+#define DIRT_RASTER_ATTR __attribute__((amdgpu_num_sgpr(80)))
 #endif
 #ifndef DIRT_RASTER_WAVES
-#define DIRT_RASTER_WAVES 7  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
-                             // the procedural programs and the generic-C path keep their natural allocation)
+#define DIRT_RASTER_WAVES 8  // min waves per SIMD the register allocation must allow (Gouraud, C = 1 or 3;
+                             // the procedural programs and the generic-C path keep their natural allocation).
+                             // 8 with <= 80 SGPRs (DIRT_RASTER_ATTR): 8 workgroups per CU, round 4
+                             // (profiles/r04/ab_raster_occupancy: raster 24.0-24.3 -> 23.6-23.8 us)
 #endif
 // Optional deferred-shading outputs of the resolve (dirt_rasterise_fwd_gbuffer; instantiated only when
 // asked for, GB = true, so the default kernel is unchanged): window depth as the DEPTH24 buffer holds it,
@@ -564,7 +566,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int lx = wave_ox(wave) + lane % kWaveW, ly = wave_oy(wave) + lane / kWaveW;
 #ifndef DIRT_RASTER_REMAT_IJ
-#define DIRT_RASTER_REMAT_IJ 0
+#define DIRT_RASTER_REMAT_IJ 1
 #endif
 #if DIRT_RASTER_REMAT_IJ
     const int i0_ = tx * kTile + lx, j0_ = ty * kTile + ly;  // (the resolve recomputes them)

@@ -248,15 +248,20 @@ def test_config4_batched_gbuffer_renders_match_three_calls():
     world, faces, albedo = dp.grid_surface(n=60)
     H = W = 256
     wts = torch.rand((H, W, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    ft, at = torch.from_numpy(faces).to(dev), torch.from_numpy(albedo).to(dev)
+    Vw = torch.from_numpy(world).to(dev)
+    three = dp.gbuffers(dp.hip_render, Vw, ft, at, H, W)[:3]
+    one = dp.gbuffers(dp.hip_render, Vw, ft, at, H, W, batched=True)[:3]
+    for a, b in zip(three, one):
+        assert torch.equal(a, b)  # the same G-buffers (-inf backgrounds included)
     res = []
     for batched in (False, True):
         Vw = torch.from_numpy(world).to(dev).requires_grad_(True)
-        L, px, valid = dp.chain(dp.hip_render, Vw, torch.from_numpy(faces).to(dev), torch.from_numpy(albedo).to(dev),
-                                H, W, wts, batched=batched)
+        L, px, valid = dp.chain(dp.hip_render, Vw, ft, at, H, W, wts, batched=batched)
         g, = torch.autograd.grad(L, [Vw])
         res.append((L.detach(), px.detach(), valid, g))
     (L0, p0, v0, g0), (L1, p1, v1, g1) = res
     assert torch.equal(v0, v1)
-    assert torch.equal(torch.where(v0, p0, torch.zeros_like(p0)), torch.where(v1, p1, torch.zeros_like(p1)))
-    torch.testing.assert_close(L1, L0, rtol=1e-6, atol=0)
+    # (the shading around the op is torch's; its kernels may round differently on differently laid out inputs)
+    torch.testing.assert_close(L1, L0, rtol=1e-5, atol=0)
     torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-5 * float(g0.abs().max()))
