@@ -465,12 +465,12 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
         zero2_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(grad_vertices, na, grad_vertex_colors, nb);
         HIP_TRY(hipGetLastError());
     }
-    // backward tiles: kGradTileW x 16 (grad_kernel.h)
-    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + kGradTileH - 1) / kGradTileH;
+    // backward tiles: kGradTileW x grad_tile_h(C) (grad_kernel.h)
+    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(C) - 1) / grad_tile_h(C);
     dim3 grid((unsigned)(gntx * gnty), (unsigned)B);
     ProfScope ps(K_GRAD, stream);
 #define LAUNCH_GRAD(CC)                                                                                       \
-    grad_kernel<CC><<<grid, dim3(GradGeom<kGradTileW>::NT), 0, stream>>>(                                      \
+    grad_kernel<CC><<<grid, dim3(GradGeom<kGradTileW, grad_tile_h(CC)>::NT), 0, stream>>>(                     \
         pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,          \
         grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H))
     if (C == 1) LAUNCH_GRAD(1);
@@ -692,8 +692,9 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, stream));
-    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + kGradTileH - 1) / kGradTileH;
-    dim3 grid((unsigned)(gntx * gnty), (unsigned)B), blk(GradGeom<kGradTileW>::NT);
+    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(C) - 1) / grad_tile_h(C);
+    dim3 grid((unsigned)(gntx * gnty), (unsigned)B), blk(C == 3 ? GradGeom<kGradTileW, grad_tile_h(3)>::NT
+                                                                : GradGeom<kGradTileW, grad_tile_h(7)>::NT);
 #define V_GRAD(AB)                                                                                                   \
     case AB:                                                                                                         \
         if (C == 3)                                                                                                  \

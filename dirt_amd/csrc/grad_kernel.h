@@ -4,7 +4,7 @@
 // ------------------------------------------------------------------------------------------------
 // K5: backward
 //
-// One workgroup per TWX x 16 tile (TWX = 16: 256 threads, TWX = 32: 512), one lane per pixel.  Every contribution of a lane goes to
+// One workgroup per TWX x TH tile (16 x 16: 256 threads; TWX = 32 or TH = 8 variants), one lane per pixel.  Every contribution of a lane goes to
 // the face visible at its own pixel: colour gradients lambda_k * G, and the share of the four
 // neighbour pairs around the pixel that this face owns (a pair's other owner is handled by the lane
 // on the other side, same-face pairs by the lower lane only).  Reduction without global contention:
@@ -107,13 +107,21 @@ struct NdcScale {
 #define DIRT_GRAD_TILE_W 16
 #endif
 constexpr int kGradTileW = DIRT_GRAD_TILE_W;
-constexpr int kGradTileH = 16;
-// staged tile with a one-pixel border: row stride TWX + 2, 18 rows
-template <int TWX>
+// Backward tile height: 16 rows (256 threads at TWX = 16) or 8 (128 threads: twice the workgroups, for frames
+// whose tile count alone does not fill the chip twice over).  RGB / one channel and the wide paths separately.
+#ifndef DIRT_GRAD_TILE_H
+#define DIRT_GRAD_TILE_H 16
+#endif
+#ifndef DIRT_GRAD_TILE_H_WIDE
+#define DIRT_GRAD_TILE_H_WIDE 16
+#endif
+__host__ __device__ constexpr int grad_tile_h(int C) { return C == 1 || C == 3 ? DIRT_GRAD_TILE_H : DIRT_GRAD_TILE_H_WIDE; }
+// staged tile with a one-pixel border: row stride TWX + 2, TH + 2 rows
+template <int TWX, int TH>
 struct GradGeom {
-    static constexpr int NT = TWX * kGradTileH;   // threads
+    static constexpr int NT = TWX * TH;           // threads
     static constexpr int HX = TWX + 2;            // staged row stride
-    static constexpr int HY = kGradTileH + 2;
+    static constexpr int HY = TH + 2;
     static constexpr int PIX = HX * HY;
 };
 constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS (typ. 10-40)
@@ -272,8 +280,8 @@ __device__ __forceinline__ int run_start(int key, int lx)  // lx: lane index wit
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
 // 32 skip the DPP run scan (every lane adds into LDS), 128 phase timestamps, 256 flush sums without
 // the global atomics
-template <int CC, int AB = 0, int TWX = kGradTileW>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
+template <int CC, int AB = 0, int TWX = kGradTileW, int TH = grad_tile_h(CC)>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
                           amdgpu_waves_per_eu(CC == 3 ? DIRT_GRAD_WAVES_C3 : DIRT_GRAD_WAVES))) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
                                                    const Rec *__restrict__ recs,
@@ -283,7 +291,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
                                                    const NdcScale ns)
 {
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
-    constexpr int NT = GradGeom<TWX>::NT, kHalo = GradGeom<TWX>::HX, kHaloPix = GradGeom<TWX>::PIX;
+    constexpr int NT = GradGeom<TWX, TH>::NT, kHalo = GradGeom<TWX, TH>::HX, kHaloPix = GradGeom<TWX, TH>::PIX;
     // LDS pixel stride: float4 for RGB, two float4 for 5..8 channels (wide LDS reads)
     constexpr int CP = CM == 3 ? 4 : (CM > 4 && CM <= 8) ? 8 : CM;
     constexpr int NVM = 9 + 3 * CM;
@@ -331,7 +339,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
     tg.split(tile, tx, ty);
     const int t = threadIdx.x, lx = t % TWX, ly = t / TWX;
     const int lr = lx & 15;  // lane within its 16-lane DPP row (a pixel row, or half of one at TWX = 32)
-    const int i = tx * TWX + lx, j = ty * kGradTileH + ly;
+    const int i = tx * TWX + lx, j = ty * TH + ly;
     const Rec *frame_recs = recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = fdata + (int64_t)b * F;
     // uniform: readfirstlane (convergent) keeps the divisions at the top instead of in every pair branch
@@ -346,7 +354,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
         s_tcnt[k] = 0;
     }
     if (t == 0) T.n = 0;
-    const int hi0 = tx * TWX - 1, hj0 = ty * kGradTileH - 1;
+    const int hi0 = tx * TWX - 1, hj0 = ty * TH - 1;
     // the staged pixels' g-buffer words and G / I (for the staged pair scalars below, !kRecompute)
     int32_t gbv[2];
     float Gv[2][CM], Iv[2][CM];
@@ -486,8 +494,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX>::NT),
                 const int k = t + NT * u;
                 if (k >= kHaloPix) continue;
                 const int hx = k % kHalo, hy = k / kHalo;
-                const bool need_x = hx <= TWX && hy >= 1 && hy <= kGradTileH;
-                const bool need_y = hx >= 1 && hx <= TWX && hy <= kGradTileH;
+                const bool need_x = hx <= TWX && hy >= 1 && hy <= TH;
+                const bool need_y = hx >= 1 && hx <= TWX && hy <= TH;
                 if (need_x) s_sx[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + 1, C);
                 if (need_y) s_sy[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + kHalo, C);
             }

@@ -20,8 +20,9 @@ def _prepare_vertices_and_faces(vertices, faces):
 
 
 def _get_face_normals(vertices, faces):
-    # vertices [*, V, 3]; result [*, F, 3] (dirt/lighting.py:23-31)
-    v = vertices[..., faces, :]  # [*, F, 3 (vertex-in-face), 3]
+    # vertices [*, V, 3]; result [*, F, 3] (dirt/lighting.py:23-31).  index_select rather than advanced
+    # indexing: its backward is one index_add, where advanced indexing's sorts the indices first
+    v = vertices.index_select(-2, faces.reshape(-1)).reshape(vertices.shape[:-2] + (faces.shape[0], 3, vertices.shape[-1]))
     normals = torch.cross(v[..., 1, :] - v[..., 0, :], v[..., 2, :] - v[..., 0, :], dim=-1)
     return normals / (torch.linalg.norm(normals, dim=-1, keepdim=True) + 1.e-12)
 
@@ -34,8 +35,8 @@ def vertex_normals(vertices, faces, name=None):
     normals_by_face = _get_face_normals(vertices, faces)  # [*, F, 3]
     lead = normals_by_face.shape[:-2]
     summed = torch.zeros(lead + (vertices.shape[-2], 3), dtype=vertices.dtype, device=vertices.device)
-    for k in range(3):
-        summed = summed.index_add(-2, faces[:, k], normals_by_face)
+    # every face's normal to its three vertices in one index_add (face-major, as faces.reshape(-1))
+    summed = summed.index_add(-2, faces.reshape(-1), normals_by_face.repeat_interleave(3, dim=-2))
     return summed / (torch.linalg.norm(summed, dim=-1, keepdim=True) + 1.e-12)
 
 
@@ -73,7 +74,8 @@ def diffuse_directional(vertex_normals, vertex_colors, light_direction, light_co
     vertex_colors = torch.as_tensor(vertex_colors, dtype=dt, device=dev)
     light_direction = torch.as_tensor(light_direction, dtype=dt, device=dev)
     light_color = torch.as_tensor(light_color, dtype=dt, device=dev)
-    cosines = torch.matmul(vertex_normals, -light_direction[..., :, None])  # [*, V, 1]
+    # (an elementwise product and a 3-term sum: a [V, 3] x [3, 1] matmul is a slow GEMM shape)
+    cosines = (vertex_normals * -light_direction[..., None, :]).sum(-1, keepdim=True)  # [*, V, 1]
     cosines = cosines.abs() if double_sided else cosines.clamp_min(0.)
     return light_color[..., None, :] * vertex_colors * cosines
 
@@ -92,7 +94,7 @@ def specular_directional(vertex_positions, vertex_normals, vertex_reflectivities
     # into a HIP graph, where such a copy is not permitted)
     shininess = shininess if isinstance(shininess, (int, float)) else as_t(shininess)[..., None, None]
     to_light = -light_direction
-    reflected = -to_light + 2. * torch.matmul(vertex_normals, to_light[..., :, None]) * vertex_normals
+    reflected = -to_light + 2. * (vertex_normals * to_light[..., None, :]).sum(-1, keepdim=True) * vertex_normals
     to_camera = camera_position[..., None, :] - vertex_positions
     cosines = ((to_camera / torch.linalg.norm(to_camera, dim=-1, keepdim=True) + 1.e-12) * reflected).sum(-1, keepdim=True)
     cosines = cosines.abs() if double_sided else cosines.clamp_min(0.)

@@ -78,21 +78,30 @@ def unit(v):
     return v / torch.linalg.norm(v)
 
 
-def gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu=False, batched=False):
+@functools.lru_cache(maxsize=16)
+def _backgrounds(H, W, device):
+    """The G-buffers' constant backgrounds (-inf for positions and normals, 0 for albedo), made once per device
+    rather than filled every step."""
+    return torch.full((H, W, 3), float("-inf"), device=device), torch.zeros((H, W, 3), device=device)
+
+
+def gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu=False, batched=False, normals=None):
     """The three G-buffer renders of samples/deferred.py:63-83 ([H,W,3] each) and the clip vertices.
 
     geometry_on_cpu: compute the clip vertices and normals on the CPU (differentiably) and move them to
     Vw's device, so that two renderers compared on two devices see bit-identical inputs.
     batched: the three renders as one rasterise_batch call of three frames sharing the geometry (the same
-    G-buffers and gradients; one op call instead of three)."""
+    G-buffers and gradients; one op call instead of three).
+    normals: precomputed vertex normals (the index_add behind lighting.vertex_normals sums with float atomics on
+    the GPU, so two computations may differ in the last bit)."""
     dev = Vw.device
     Vx = Vw.cpu() if geometry_on_cpu else Vw
     view, proj = camera(H, W, Vx.device)
     Vh = torch.cat([Vx, torch.ones_like(Vx[:, :1])], 1)
     clip = (Vh @ view @ proj).to(dev)
-    normals = lighting.vertex_normals(Vx, faces.to(Vx.device).long()).to(dev)
-    ninf = torch.full((H, W, 3), float("-inf"), device=dev)
-    zero = torch.zeros((H, W, 3), device=dev)
+    if normals is None:
+        normals = lighting.vertex_normals(Vx, faces.to(Vx.device).long()).to(dev)
+    ninf, zero = _backgrounds(H, W, dev)
     if batched:
         import dirt_amd
         bg = torch.stack([ninf, zero, ninf])

@@ -17,6 +17,7 @@ import pytest
 import torch
 
 import deferred_pipeline as dp
+from dirt_amd import lighting
 import scenes
 from oracle import oracle
 from test_gpu_parity import assert_close_grad, check_scene, _gpu
@@ -250,8 +251,10 @@ def test_config4_batched_gbuffer_renders_match_three_calls():
     wts = torch.rand((H, W, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(3))
     ft, at = torch.from_numpy(faces).to(dev), torch.from_numpy(albedo).to(dev)
     Vw = torch.from_numpy(world).to(dev)
-    three = dp.gbuffers(dp.hip_render, Vw, ft, at, H, W)[:3]
-    one = dp.gbuffers(dp.hip_render, Vw, ft, at, H, W, batched=True)[:3]
+    # one set of vertex normals for both (their index_add sums with float atomics: not bit-reproducible)
+    nrm = lighting.vertex_normals(Vw, ft.long())
+    three = dp.gbuffers(dp.hip_render, Vw, ft, at, H, W, normals=nrm)[:3]
+    one = dp.gbuffers(dp.hip_render, Vw, ft, at, H, W, batched=True, normals=nrm)[:3]
     for a, b in zip(three, one):
         assert torch.equal(a, b)  # the same G-buffers (-inf backgrounds included)
     res = []
