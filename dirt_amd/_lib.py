@@ -27,7 +27,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes
@@ -56,6 +56,12 @@ SIGNATURES = {
     "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
     "dirt_profile_enable": (_I, [_I]),
     "dirt_profile_read": (_I, [_I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double)]),
+    "dirt_vertex_normals_fwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "dirt_vertex_normals_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
+    "dirt_diffuse_directional_fwd": (_I, [_P, _P, _I64, _P, _P, _I, _P, _P]),
+    "dirt_diffuse_directional_bwd": (_I, [_P, _P, _I64, _P, _P, _I, _P, _P, _P, _P]),
+    "dirt_specular_directional_fwd": (_I, [_P, _P, _P, _I64, _P, _P, _P, ctypes.c_float, _I, _P, _P]),
+    "dirt_specular_directional_bwd": (_I, [_P, _P, _P, _I64, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _P]),
     "dirt_last_error": (ctypes.c_char_p, []),
 }
 

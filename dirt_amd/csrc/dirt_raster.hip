@@ -193,6 +193,7 @@ int validate(int B, int H, int W, int C, int V, int F)
 #include "setup_kernel.h"
 #include "raster_kernel.h"
 #include "grad_kernel.h"
+#include "lighting_kernels.h"
 
 // zero two float arrays in one launch (the backward's atomically accumulated outputs)
 __global__ __launch_bounds__(256) void zero2_kernel(float *__restrict__ a, int64_t na, float *__restrict__ b, int64_t nb)
@@ -244,7 +245,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 8; }
+int dirt_abi_version(void) { return 9; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -805,6 +806,114 @@ int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, s
     HIP_TRY(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     if (h) return fail(DIRT_EFACE, "Rasterise: face index out of range [0, vertex count)");
+    return DIRT_OK;
+}
+
+
+// ---- fused lighting helpers (lighting_kernels.h; dirt/lighting.py)
+
+int dirt_vertex_normals_fwd(const float *vertices, int vertex_stride, const void *faces, int faces_int64, int B, int V,
+                            int F, float *summed, float *normals, void *stream_)
+{
+    if (B < 0 || V < 0 || F < 0 || vertex_stride < 3)
+        return fail(DIRT_EINVAL, "vertex_normals: negative size or vertex stride < 3");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const int64_t nv = (int64_t)B * V;
+    if (nv == 0) return DIRT_OK;
+    HIP_TRY(hipMemsetAsync(summed, 0, (size_t)nv * 3 * sizeof(float), stream));
+    if (F > 0 && B > 0) {
+        const dim3 grid(light_blocks(F), (unsigned)B);
+        if (faces_int64)
+            vnormals_face_kernel<int64_t><<<grid, dim3(kLightThreads), 0, stream>>>(
+                vertices, vertex_stride, static_cast<const int64_t *>(faces), V, F, summed);
+        else
+            vnormals_face_kernel<int32_t><<<grid, dim3(kLightThreads), 0, stream>>>(
+                vertices, vertex_stride, static_cast<const int32_t *>(faces), V, F, summed);
+        HIP_TRY(hipGetLastError());
+    }
+    vnormals_vertex_kernel<<<dim3(light_blocks(nv)), dim3(kLightThreads), 0, stream>>>(summed, nv, normals);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_vertex_normals_bwd(const float *vertices, int vertex_stride, const void *faces, int faces_int64, int B, int V,
+                            int F, const float *summed, const float *grad_normals, float *grad_summed,
+                            float *grad_vertices, int grad_stride, void *stream_)
+{
+    if (B < 0 || V < 0 || F < 0 || vertex_stride < 3 || grad_stride < 3)
+        return fail(DIRT_EINVAL, "vertex_normals: negative size or vertex stride < 3");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const int64_t nv = (int64_t)B * V;
+    if (nv == 0) return DIRT_OK;
+    HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)nv * grad_stride * sizeof(float), stream));
+    if (F == 0) return DIRT_OK;
+    vnormals_vertex_bwd_kernel<<<dim3(light_blocks(nv)), dim3(kLightThreads), 0, stream>>>(summed, grad_normals, nv,
+                                                                                          grad_summed);
+    HIP_TRY(hipGetLastError());
+    const dim3 grid(light_blocks(F), (unsigned)B);
+    if (faces_int64)
+        vnormals_face_bwd_kernel<int64_t><<<grid, dim3(kLightThreads), 0, stream>>>(
+            vertices, vertex_stride, static_cast<const int64_t *>(faces), V, F, grad_summed, grad_vertices, grad_stride);
+    else
+        vnormals_face_bwd_kernel<int32_t><<<grid, dim3(kLightThreads), 0, stream>>>(
+            vertices, vertex_stride, static_cast<const int32_t *>(faces), V, F, grad_summed, grad_vertices, grad_stride);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_diffuse_directional_fwd(const float *normals, const float *colors, int64_t N, const float *light_direction,
+                                 const float *light_color, int double_sided, float *out, void *stream_)
+{
+    if (N < 0) return fail(DIRT_EINVAL, "diffuse_directional: negative size");
+    if (N == 0) return DIRT_OK;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    diffuse_fwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(normals, colors, N, light_direction,
+                                                                                  light_color, double_sided, out);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_diffuse_directional_bwd(const float *normals, const float *colors, int64_t N, const float *light_direction,
+                                 const float *light_color, int double_sided, const float *grad_out,
+                                 float *grad_normals, float *grad_colors, void *stream_)
+{
+    if (N < 0) return fail(DIRT_EINVAL, "diffuse_directional: negative size");
+    if (N == 0 || (!grad_normals && !grad_colors)) return DIRT_OK;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    diffuse_bwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
+        normals, colors, N, light_direction, light_color, double_sided, grad_out, grad_normals, grad_colors);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_specular_directional_fwd(const float *positions, const float *normals, const float *reflectivities, int64_t N,
+                                  const float *light_direction, const float *light_color,
+                                  const float *camera_position, float shininess, int double_sided, float *out,
+                                  void *stream_)
+{
+    if (N < 0) return fail(DIRT_EINVAL, "specular_directional: negative size");
+    if (N == 0) return DIRT_OK;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    specular_fwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
+        positions, normals, reflectivities, N, light_direction, light_color, camera_position, shininess, double_sided,
+        out);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_specular_directional_bwd(const float *positions, const float *normals, const float *reflectivities, int64_t N,
+                                  const float *light_direction, const float *light_color,
+                                  const float *camera_position, float shininess, int double_sided,
+                                  const float *grad_out, float *grad_positions, float *grad_normals,
+                                  float *grad_reflectivities, void *stream_)
+{
+    if (N < 0) return fail(DIRT_EINVAL, "specular_directional: negative size");
+    if (N == 0 || (!grad_positions && !grad_normals && !grad_reflectivities)) return DIRT_OK;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    specular_bwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
+        positions, normals, reflectivities, N, light_direction, light_color, camera_position, shininess, double_sided,
+        grad_out, grad_positions, grad_normals, grad_reflectivities);
+    HIP_TRY(hipGetLastError());
     return DIRT_OK;
 }
 

@@ -34,6 +34,12 @@ struct Api {
     decltype(&dirt_scratch_clear) scratch_clear = nullptr;
     decltype(&dirt_check_faces) check_faces = nullptr;
     decltype(&dirt_last_error) last_error = nullptr;
+    decltype(&dirt_vertex_normals_fwd) vn_fwd = nullptr;
+    decltype(&dirt_vertex_normals_bwd) vn_bwd = nullptr;
+    decltype(&dirt_diffuse_directional_fwd) diffuse_fwd = nullptr;
+    decltype(&dirt_diffuse_directional_bwd) diffuse_bwd = nullptr;
+    decltype(&dirt_specular_directional_fwd) specular_fwd = nullptr;
+    decltype(&dirt_specular_directional_bwd) specular_bwd = nullptr;
 } g_api;
 
 void check(int rc)
@@ -61,6 +67,12 @@ void init(const std::string &path)
     g_api.scratch_clear = reinterpret_cast<decltype(g_api.scratch_clear)>(sym("dirt_scratch_clear"));
     g_api.check_faces = reinterpret_cast<decltype(g_api.check_faces)>(sym("dirt_check_faces"));
     g_api.last_error = reinterpret_cast<decltype(g_api.last_error)>(sym("dirt_last_error"));
+    g_api.vn_fwd = reinterpret_cast<decltype(g_api.vn_fwd)>(sym("dirt_vertex_normals_fwd"));
+    g_api.vn_bwd = reinterpret_cast<decltype(g_api.vn_bwd)>(sym("dirt_vertex_normals_bwd"));
+    g_api.diffuse_fwd = reinterpret_cast<decltype(g_api.diffuse_fwd)>(sym("dirt_diffuse_directional_fwd"));
+    g_api.diffuse_bwd = reinterpret_cast<decltype(g_api.diffuse_bwd)>(sym("dirt_diffuse_directional_bwd"));
+    g_api.specular_fwd = reinterpret_cast<decltype(g_api.specular_fwd)>(sym("dirt_specular_directional_fwd"));
+    g_api.specular_bwd = reinterpret_cast<decltype(g_api.specular_bwd)>(sym("dirt_specular_directional_bwd"));
 }
 
 // Forward-only scratch (bins, bin counters) per (device, stream, layout), cleared once: every forward
@@ -310,6 +322,119 @@ variable_list rasterise_checked(at::Tensor background, at::Tensor vertices, at::
                      bin_capacity, want_gbuf, check_faces, fwd_flags);
 }
 
+// ---- fused lighting helpers (dirt/lighting.py; dirt_amd/lighting.py decides when they apply: CUDA float32
+// tensors, [..., 3] operands of one shape, light parameters of shape [3] that need no gradient)
+
+hipStream_t stream_of(const at::Tensor &x)
+{
+    return c10::hip::getCurrentHIPStream(x.device().index()).stream();
+}
+
+at::Tensor grad_or_zeros(const at::Tensor &g, const at::Tensor &like)
+{
+    return g.defined() ? g.to(at::kFloat).contiguous() : at::zeros_like(like);
+}
+
+struct VertexNormalsFn : public torch::autograd::Function<VertexNormalsFn> {
+    // vertices [*, V, D >= 3] contiguous (only x, y, z read), faces [F, 3] int32 / int64
+    static at::Tensor forward(AutogradContext *ctx, at::Tensor vertices, at::Tensor faces)
+    {
+        c10::hip::HIPGuard guard(vertices.device().index());
+        const int64_t V = vertices.size(-2), F = faces.size(0), B = vertices.numel() / std::max<int64_t>(V * vertices.size(-1), 1);
+        std::vector<int64_t> shape = vertices.sizes().vec();
+        shape.back() = 3;
+        at::Tensor summed = at::empty(shape, vertices.options()), normals = at::empty(shape, vertices.options());
+        check(g_api.vn_fwd(vertices.data_ptr<float>(), (int)vertices.size(-1), faces.data_ptr(),
+                           faces.scalar_type() == at::kLong, (int)B, (int)V, (int)F, summed.data_ptr<float>(),
+                           normals.data_ptr<float>(), stream_of(vertices)));
+        ctx->save_for_backward({vertices, faces, summed});
+        return normals;
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list grads)
+    {
+        auto sv = ctx->get_saved_variables();
+        const at::Tensor &vertices = sv[0], &faces = sv[1], &summed = sv[2];
+        c10::hip::HIPGuard guard(vertices.device().index());
+        const int64_t V = vertices.size(-2), F = faces.size(0), D = vertices.size(-1);
+        const int64_t B = vertices.numel() / std::max<int64_t>(V * D, 1);
+        at::Tensor g = grad_or_zeros(grads[0], summed);
+        at::Tensor gsum = at::empty_like(summed), gv = at::empty(vertices.sizes(), vertices.options());
+        check(g_api.vn_bwd(vertices.data_ptr<float>(), (int)D, faces.data_ptr(), faces.scalar_type() == at::kLong,
+                           (int)B, (int)V, (int)F, summed.data_ptr<float>(), g.data_ptr<float>(),
+                           gsum.data_ptr<float>(), gv.data_ptr<float>(), (int)D, stream_of(vertices)));
+        return {gv, at::Tensor()};
+    }
+};
+
+struct DiffuseFn : public torch::autograd::Function<DiffuseFn> {
+    static at::Tensor forward(AutogradContext *ctx, at::Tensor normals, at::Tensor colors, at::Tensor light_direction,
+                              at::Tensor light_color, bool double_sided)
+    {
+        c10::hip::HIPGuard guard(normals.device().index());
+        at::Tensor out = at::empty_like(normals);
+        check(g_api.diffuse_fwd(normals.data_ptr<float>(), colors.data_ptr<float>(), normals.numel() / 3,
+                                light_direction.data_ptr<float>(), light_color.data_ptr<float>(), double_sided,
+                                out.data_ptr<float>(), stream_of(normals)));
+        ctx->save_for_backward({normals, colors, light_direction, light_color});
+        ctx->saved_data["two"] = double_sided;
+        return out;
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list grads)
+    {
+        auto sv = ctx->get_saved_variables();
+        const at::Tensor &normals = sv[0], &colors = sv[1];
+        c10::hip::HIPGuard guard(normals.device().index());
+        at::Tensor g = grad_or_zeros(grads[0], normals);
+        const bool wn = ctx->needs_input_grad(0), wc = ctx->needs_input_grad(1);
+        at::Tensor gn = wn ? at::empty_like(normals) : at::Tensor(), gc = wc ? at::empty_like(colors) : at::Tensor();
+        check(g_api.diffuse_bwd(normals.data_ptr<float>(), colors.data_ptr<float>(), normals.numel() / 3,
+                                sv[2].data_ptr<float>(), sv[3].data_ptr<float>(), ctx->saved_data["two"].toBool(),
+                                g.data_ptr<float>(), wn ? gn.data_ptr<float>() : nullptr,
+                                wc ? gc.data_ptr<float>() : nullptr, stream_of(normals)));
+        return {gn, gc, at::Tensor(), at::Tensor(), at::Tensor()};
+    }
+};
+
+struct SpecularFn : public torch::autograd::Function<SpecularFn> {
+    static at::Tensor forward(AutogradContext *ctx, at::Tensor positions, at::Tensor normals, at::Tensor reflectivities,
+                              at::Tensor light_direction, at::Tensor light_color, at::Tensor camera_position,
+                              double shininess, bool double_sided)
+    {
+        c10::hip::HIPGuard guard(positions.device().index());
+        at::Tensor out = at::empty_like(positions);
+        check(g_api.specular_fwd(positions.data_ptr<float>(), normals.data_ptr<float>(), reflectivities.data_ptr<float>(),
+                                 positions.numel() / 3, light_direction.data_ptr<float>(), light_color.data_ptr<float>(),
+                                 camera_position.data_ptr<float>(), (float)shininess, double_sided,
+                                 out.data_ptr<float>(), stream_of(positions)));
+        ctx->save_for_backward({positions, normals, reflectivities, light_direction, light_color, camera_position});
+        ctx->saved_data["two"] = double_sided;
+        ctx->saved_data["shininess"] = shininess;
+        return out;
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list grads)
+    {
+        auto sv = ctx->get_saved_variables();
+        const at::Tensor &positions = sv[0], &normals = sv[1], &refl = sv[2];
+        c10::hip::HIPGuard guard(positions.device().index());
+        at::Tensor g = grad_or_zeros(grads[0], positions);
+        const bool wp = ctx->needs_input_grad(0), wn = ctx->needs_input_grad(1), wr = ctx->needs_input_grad(2);
+        at::Tensor gp = wp ? at::empty_like(positions) : at::Tensor(), gn = wn ? at::empty_like(normals) : at::Tensor(),
+                   gr = wr ? at::empty_like(refl) : at::Tensor();
+        check(g_api.specular_bwd(positions.data_ptr<float>(), normals.data_ptr<float>(), refl.data_ptr<float>(),
+                                 positions.numel() / 3, sv[3].data_ptr<float>(), sv[4].data_ptr<float>(),
+                                 sv[5].data_ptr<float>(), (float)ctx->saved_data["shininess"].toDouble(),
+                                 ctx->saved_data["two"].toBool(), g.data_ptr<float>(),
+                                 wp ? gp.data_ptr<float>() : nullptr, wn ? gn.data_ptr<float>() : nullptr,
+                                 wr ? gr.data_ptr<float>() : nullptr, stream_of(positions)));
+        return {gp, gn, gr, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
+    }
+};
+
+void need_api()
+{
+    if (!g_api.vn_fwd) throw std::runtime_error("_dirt_torch.init(path) was not called");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
@@ -327,4 +452,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
           py::arg("fwd_flags") = (int64_t)DIRT_FWD_SCRATCH_CLEAN);
     m.def("scratch_cache_clear", [](bool force) { g_scratch.clear(force); }, py::arg("force") = false);
     m.def("scratch_cache_size", []() { return g_scratch.size(); });
+    // fused lighting helpers: operands already CUDA float32 and contiguous (dirt_amd/lighting.py checks)
+    m.def("vertex_normals", [](at::Tensor vertices, at::Tensor faces) {
+        need_api();
+        return VertexNormalsFn::apply(vertices, faces);
+    });
+    m.def("diffuse_directional", [](at::Tensor n, at::Tensor c, at::Tensor ld, at::Tensor lc, bool two) {
+        need_api();
+        return DiffuseFn::apply(n, c, ld, lc, two);
+    });
+    m.def("specular_directional", [](at::Tensor p, at::Tensor n, at::Tensor r, at::Tensor ld, at::Tensor lc,
+                                     at::Tensor cam, double shininess, bool two) {
+        need_api();
+        return SpecularFn::apply(p, n, r, ld, lc, cam, shininess, two);
+    });
 }

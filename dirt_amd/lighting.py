@@ -4,6 +4,13 @@ Functions, arguments and formulas follow dirt/lighting.py:34-344.  They generate
 Gouraud (direct) shading or shade a G-buffer (deferred shading, samples/deferred.py:93-120) and are
 differentiable through torch autograd, so gradients flow from pixels through the rasterise op into
 normals and geometry (BASELINE config 4: "gradient through normals").
+
+On the GPU, vertex_normals, diffuse_directional and specular_directional run as fused HIP kernels (one launch
+per forward and per backward, dirt_amd/csrc/lighting_kernels.h, C ABI dirt_vertex_normals_* /
+dirt_diffuse_directional_* / dirt_specular_directional_*) when their operands are float32 tensors on one GPU,
+of one [..., 3] shape, with light parameters of shape [3] that need no gradient and a Python-number
+shininess; anything else -- CPU tensors, broadcasting, gradients with respect to the light -- runs the
+framework-op statement below (`_*_ops`), which is also the fused kernels' fp32 test reference.
 """
 import torch
 
@@ -27,10 +34,44 @@ def _get_face_normals(vertices, faces):
     return normals / (torch.linalg.norm(normals, dim=-1, keepdim=True) + 1.e-12)
 
 
+def _fused():
+    """The C++ extension bound to the HIP library (None if not built: the framework ops run)."""
+    from .rasterise_ops import _torch_ext
+    return _torch_ext()
+
+
+def _gpu_f32(*xs):
+    x0 = xs[0]
+    return (x0.is_cuda and all(isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.device == x0.device
+                               for x in xs))
+
+
+def _light_param(x, like):
+    """A [3] light parameter usable by the fused kernels (on like's device, float32, no gradient), else None."""
+    if not isinstance(x, torch.Tensor) or x.shape != (3,) or x.dtype != torch.float32 or x.device != like.device:
+        return None
+    if x.requires_grad and torch.is_grad_enabled():
+        return None
+    return x.contiguous()
+
+
 def vertex_normals(vertices, faces, name=None):
     """Normalised average of the normals of the faces around each vertex (dirt/lighting.py:34-98)."""
     del name
+    vertices = torch.as_tensor(vertices)
+    f = torch.as_tensor(faces, device=vertices.device)
+    if (_gpu_f32(vertices) and vertices.dim() >= 2 and vertices.shape[-1] >= 3 and f.dim() == 2 and
+            f.shape[-1] == 3 and f.dtype in (torch.int32, torch.int64)):
+        ext = _fused()
+        if ext is not None:
+            # (int32 or int64 faces as given; a face with an index outside [0, V) contributes nothing here,
+            # where the framework ops raise)
+            return ext.vertex_normals(vertices.contiguous(), f.contiguous())
     vertices, faces = _prepare_vertices_and_faces(vertices, faces)
+    return _vertex_normals_ops(vertices, faces)
+
+
+def _vertex_normals_ops(vertices, faces):
     vertices = vertices[..., :3]
     normals_by_face = _get_face_normals(vertices, faces)  # [*, F, 3]
     lead = normals_by_face.shape[:-2]
@@ -72,6 +113,18 @@ def diffuse_directional(vertex_normals, vertex_colors, light_direction, light_co
     vertex_normals = torch.as_tensor(vertex_normals)
     dev, dt = vertex_normals.device, vertex_normals.dtype
     vertex_colors = torch.as_tensor(vertex_colors, dtype=dt, device=dev)
+    if (_gpu_f32(vertex_normals, vertex_colors) and vertex_normals.shape[-1:] == (3,) and
+            vertex_colors.shape == vertex_normals.shape):
+        ld, lc = _light_param(light_direction, vertex_normals), _light_param(light_color, vertex_normals)
+        ext = _fused() if ld is not None and lc is not None else None
+        if ext is not None:
+            return ext.diffuse_directional(vertex_normals.contiguous(), vertex_colors.contiguous(), ld, lc,
+                                           bool(double_sided))
+    return _diffuse_directional_ops(vertex_normals, vertex_colors, light_direction, light_color, double_sided)
+
+
+def _diffuse_directional_ops(vertex_normals, vertex_colors, light_direction, light_color, double_sided):
+    dev, dt = vertex_normals.device, vertex_normals.dtype
     light_direction = torch.as_tensor(light_direction, dtype=dt, device=dev)
     light_color = torch.as_tensor(light_color, dtype=dt, device=dev)
     # (an elementwise product and a 3-term sum: a [V, 3] x [3, 1] matmul is a slow GEMM shape)
@@ -88,6 +141,23 @@ def specular_directional(vertex_positions, vertex_normals, vertex_reflectivities
     dev, dt = vertex_positions.device, vertex_positions.dtype
     as_t = lambda x: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
     vertex_normals, vertex_reflectivities = as_t(vertex_normals), as_t(vertex_reflectivities)
+    if (_gpu_f32(vertex_positions, vertex_normals, vertex_reflectivities) and vertex_positions.shape[-1:] == (3,) and
+            vertex_normals.shape == vertex_positions.shape and vertex_reflectivities.shape == vertex_positions.shape and
+            isinstance(shininess, (int, float))):
+        ps = [_light_param(x, vertex_positions) for x in (light_direction, light_color, camera_position)]
+        ext = _fused() if all(p is not None for p in ps) else None
+        if ext is not None:
+            return ext.specular_directional(vertex_positions.contiguous(), vertex_normals.contiguous(),
+                                            vertex_reflectivities.contiguous(), ps[0], ps[1], ps[2], float(shininess),
+                                            bool(double_sided))
+    return _specular_directional_ops(vertex_positions, vertex_normals, vertex_reflectivities, light_direction,
+                                     light_color, camera_position, shininess, double_sided)
+
+
+def _specular_directional_ops(vertex_positions, vertex_normals, vertex_reflectivities, light_direction, light_color,
+                              camera_position, shininess, double_sided):
+    dev, dt = vertex_positions.device, vertex_positions.dtype
+    as_t = lambda x: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
     light_direction, light_color = as_t(light_direction), as_t(light_color)
     camera_position = as_t(camera_position)
     # a Python-number exponent stays a number: no host-to-device copy per call (and the call can be captured

@@ -72,7 +72,8 @@ extern "C" {
 /* ABI version, bumped on any signature or workspace-layout change (4: + dirt_hill_fwd, shader ids 6 and 7;
  * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
  * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer; 8: + dirt_rasterise_bwd_recompute,
- * dirt_bwd_recompute_workspace_size) */
+ * dirt_bwd_recompute_workspace_size; 9: + the fused lighting helpers dirt_vertex_normals_*,
+ * dirt_diffuse_directional_*, dirt_specular_directional_*) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -188,6 +189,44 @@ int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, s
 #define DIRT_NUM_KERNELS 3
 int dirt_profile_enable(int enable);
 int dirt_profile_read(int kernel_id, const char **name, int *launches, double *total_ms);
+
+/* Fused lighting helpers: dirt/lighting.py's vertex_normals (:34-98), diffuse_directional (:182-225) and
+ * specular_directional (:228-288) -- TensorFlow compositions in the reference (no op of librasterise.so), one
+ * kernel per forward / backward here (the deferred-shading chain of samples/deferred.py:62-118 runs them per
+ * pixel).  Formulas: dirt_amd/lighting.py.  Light parameters are DEVICE pointers to 3 floats; gradients with
+ * respect to them are not computed (the Python layer uses its framework-op statement when they are needed).
+ * Backward rules at the kinks as the framework's: d|x| = sign(x) (0 at 0), max(x, 0) passes where x >= 0.
+ *
+ * vertex_normals: vertices [B,V,vertex_stride] (x, y, z first; stride >= 3), faces [F,3] shared by the B
+ * frames (int32, or int64 when faces_int64), out-of-range faces skipped.  summed [B,V,3] (zeroed by the call)
+ * is the unnormalised sum the backward needs; normals [B,V,3].  The sums use float atomics: the result may
+ * differ in the last bit between calls (as the framework's index_add on a GPU).
+ * The backward zero-fills grad_vertices [B,V,grad_stride] and accumulates into its first 3 components;
+ * grad_summed [B,V,3] is scratch. */
+int dirt_vertex_normals_fwd(const float *vertices, int vertex_stride, const void *faces, int faces_int64, int B, int V,
+                            int F, float *summed, float *normals, void *stream);
+int dirt_vertex_normals_bwd(const float *vertices, int vertex_stride, const void *faces, int faces_int64, int B, int V,
+                            int F, const float *summed, const float *grad_normals, float *grad_summed,
+                            float *grad_vertices, int grad_stride, void *stream);
+/* diffuse_directional: normals, colors, out [N,3]; out = light_color * colors * clamp(normals . -light_direction).
+ * Backward: grad_normals / grad_colors [N,3] overwritten (either may be NULL). */
+int dirt_diffuse_directional_fwd(const float *normals, const float *colors, int64_t N, const float *light_direction,
+                                 const float *light_color, int double_sided, float *out, void *stream);
+int dirt_diffuse_directional_bwd(const float *normals, const float *colors, int64_t N, const float *light_direction,
+                                 const float *light_color, int double_sided, const float *grad_out,
+                                 float *grad_normals, float *grad_colors, void *stream);
+/* specular_directional: positions, normals, reflectivities, out [N,3]; Phong lobe around the reflected light
+ * direction, out = light_color * reflectivities * clamp(cos)^shininess.  Backward: the three input gradients
+ * [N,3] overwritten (each may be NULL). */
+int dirt_specular_directional_fwd(const float *positions, const float *normals, const float *reflectivities, int64_t N,
+                                  const float *light_direction, const float *light_color,
+                                  const float *camera_position, float shininess, int double_sided, float *out,
+                                  void *stream);
+int dirt_specular_directional_bwd(const float *positions, const float *normals, const float *reflectivities, int64_t N,
+                                  const float *light_direction, const float *light_color,
+                                  const float *camera_position, float shininess, int double_sided,
+                                  const float *grad_out, float *grad_positions, float *grad_normals,
+                                  float *grad_reflectivities, void *stream);
 
 /* Thread-local message for the last non-OK return on this thread. */
 const char *dirt_last_error(void);

@@ -127,8 +127,7 @@ def shade(pos, col, nrm, H, W):
     pos_d = torch.where(bgmask, dilate(pos), pos)
     nrm_d = torch.where(bgmask, dilate(nrm), nrm)
     valid = torch.isfinite(pos_d).all(-1, keepdim=True) & torch.isfinite(nrm_d).all(-1, keepdim=True)
-    zero = torch.zeros_like(pos_d)
-    pos_s, nrm_s, col_s = (torch.where(valid, x, zero) for x in (pos_d, nrm_d, col))
+    pos_s, nrm_s, col_s = (torch.where(valid, x, 0.0) for x in (pos_d, nrm_d, col))
     grey, light_direction, red, white = _constants(dev)
     ambient = col_s * grey
     diffuse = lighting.diffuse_directional(nrm_s.reshape(-1, 3), col_s.reshape(-1, 3), light_direction,
@@ -143,7 +142,7 @@ def shade(pos, col, nrm, H, W):
 
 def loss_fn(pixels, valid, weights, mask=None):
     m = valid if mask is None else (valid & mask)
-    return torch.where(m, pixels * weights, torch.zeros_like(pixels)).sum()
+    return torch.where(m, pixels * weights, 0.0).sum()
 
 
 def chain(render, Vw, faces, albedo, H, W, weights, mask=None, geometry_on_cpu=False, batched=False):
