@@ -431,8 +431,9 @@ def rasterise(background, vertices, vertex_colors, faces, camera_pos=None, heigh
     vertices = _as_tensor(vertices, torch.float32, dev)
     vertex_colors = _as_tensor(vertex_colors, torch.float32, dev)
     faces = _as_tensor(faces, torch.int32, dev)
+    # (squeeze, not [0]: the gradient of a select is a zero-filled batch plus a copy, a squeeze's is a view)
     return _rasterise_batched(background[None], vertices[None], vertex_colors[None], faces[None], camera_pos,
-                              height, width, channels, _shader_id(shader), check_faces=check_faces)[0]
+                              height, width, channels, _shader_id(shader), check_faces=check_faces).squeeze(0)
 
 
 def rasterise_batch(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
@@ -492,7 +493,7 @@ def rasterise_gbuffer(background, vertices, vertex_colors, faces, height=None, w
                                 _as_tensor(vertex_colors, torch.float32, dev)[None],
                                 _as_tensor(faces, torch.int32, dev)[None], height, width, channels,
                                 check_faces=check_faces)
-    return GBuffer(*(t[0] for t in g))
+    return GBuffer(*(t.squeeze(0) for t in g))
 
 
 def _procedural_op(opname, shader, ref):

@@ -51,14 +51,14 @@ def _camera_cpu(H, W):
 @functools.lru_cache(maxsize=16)
 def _camera_on(H, W, device):
     view, proj, pos = _camera_cpu(H, W)
-    return view.to(device), proj.to(device), pos.to(device)
+    return view.to(device), proj.to(device), pos.to(device), (view @ proj).to(device)
 
 
 def camera(H, W, device=None):
     """The sample's camera (samples/deferred.py:50-60, OpenGL perspective); the surface is tilted towards the
     camera (rotation about x) and pushed away along -z.  Built once on the CPU, moved once per device (so a
     step can be captured into a HIP graph: no host-to-device copy inside it)."""
-    view, proj, _ = _camera_on(H, W, torch.device(device) if device is not None else torch.device("cpu"))
+    view, proj = _camera_on(H, W, torch.device(device) if device is not None else torch.device("cpu"))[:2]
     return view, proj
 
 
@@ -96,11 +96,12 @@ def gbuffers(render, Vw, faces, albedo, H, W, geometry_on_cpu=False, batched=Fal
     the GPU, so two computations may differ in the last bit)."""
     dev = Vw.device
     Vx = Vw.cpu() if geometry_on_cpu else Vw
-    view, proj = camera(H, W, Vx.device)
-    Vh = torch.cat([Vx, torch.ones_like(Vx[:, :1])], 1)
-    clip = (Vh @ view @ proj).to(dev)
+    # clip = [Vx, 1] @ view @ proj (samples/deferred.py:50-60), as one addmm with the camera's product
+    # view @ proj precomputed: the homogeneous 1 picks its last row
+    vp = _camera_on(H, W, Vx.device)[3]
+    clip = torch.addmm(vp[3], Vx, vp[:3]).to(dev)
     if normals is None:
-        normals = lighting.vertex_normals(Vx, faces.to(Vx.device).long()).to(dev)
+        normals = lighting.vertex_normals(Vx, faces.to(Vx.device)).to(dev)
     ninf, zero = _backgrounds(H, W, dev)
     if batched:
         import dirt_amd
