@@ -85,6 +85,15 @@ def test_recompute_fuzz_batch_clipped_channels_small_and_empty():
     assert np.all(r["grad_vertices"] == 0.0) and np.all(r["grad_colors"] == 0.0)
 
 
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_RC_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_RC_FUZZ_SEEDS", "6"))))
+def test_recompute_fuzz_adversarial_scenes(seed):
+    """The recompute backward on the adversarial fuzz batches of test_gpu_parity.py (scenes.fuzz_case: clipping,
+    w <= 0, slivers, ties, guard-band overflow, channel counts 1..7): the same gradients as the stateful
+    backward and the oracle.  DIRT_RC_FUZZ_SEEDS=N widens it (default 6), from DIRT_RC_FUZZ_FIRST."""
+    check_both(*scenes.fuzz_case(200000 + seed), seed=seed)
+
+
 def test_reference_wrapper_body_runs_unchanged():
     """dirt/rasterise_ops.py:39-54 with TF's calls mapped to torch: the op module's single output is indexed
     with [0], exactly as the reference does; the gradient is registered (the fork has none)."""
