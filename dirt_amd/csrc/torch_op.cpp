@@ -435,6 +435,23 @@ void need_api()
     if (!g_api.vn_fwd) throw std::runtime_error("_dirt_torch.init(path) was not called");
 }
 
+// the fused helpers take raw device pointers: every operand on the first one's GPU, float32 (or int faces),
+// contiguous, with the element counts the kernels index by (dirt_amd/lighting.py checks this before calling)
+void check_operands(const char *fn, std::initializer_list<const at::Tensor *> xs, std::initializer_list<const at::Tensor *> params)
+{
+    const at::Tensor &x0 = **xs.begin();
+    auto bad = [&](const char *what) { throw std::invalid_argument(std::string(fn) + ": " + what); };
+    if (!x0.is_cuda()) bad("operands must be GPU tensors");
+    for (const at::Tensor *x : xs) {
+        if (x->device() != x0.device() || x->scalar_type() != at::kFloat || !x->is_contiguous())
+            bad("operands must be contiguous float32 tensors on one GPU");
+        if (x->sizes() != x0.sizes() || x->dim() < 1 || x->size(-1) != 3) bad("operands must share one [..., 3] shape");
+    }
+    for (const at::Tensor *p : params)
+        if (p->device() != x0.device() || p->scalar_type() != at::kFloat || !p->is_contiguous() || p->numel() != 3)
+            bad("light parameters must be contiguous float32 [3] tensors on the operands' GPU");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
@@ -455,15 +472,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
     // fused lighting helpers: operands already CUDA float32 and contiguous (dirt_amd/lighting.py checks)
     m.def("vertex_normals", [](at::Tensor vertices, at::Tensor faces) {
         need_api();
+        if (!vertices.is_cuda() || vertices.scalar_type() != at::kFloat || !vertices.is_contiguous() ||
+            vertices.dim() < 2 || vertices.size(-1) < 3)
+            throw std::invalid_argument("vertex_normals: vertices must be a contiguous float32 [..., V, >=3] GPU tensor");
+        if (faces.device() != vertices.device() || !faces.is_contiguous() || faces.dim() != 2 || faces.size(1) != 3 ||
+            (faces.scalar_type() != at::kInt && faces.scalar_type() != at::kLong))
+            throw std::invalid_argument("vertex_normals: faces must be a contiguous int32 / int64 [F, 3] tensor on the vertices' GPU");
         return VertexNormalsFn::apply(vertices, faces);
     });
     m.def("diffuse_directional", [](at::Tensor n, at::Tensor c, at::Tensor ld, at::Tensor lc, bool two) {
         need_api();
+        check_operands("diffuse_directional", {&n, &c}, {&ld, &lc});
         return DiffuseFn::apply(n, c, ld, lc, two);
     });
     m.def("specular_directional", [](at::Tensor p, at::Tensor n, at::Tensor r, at::Tensor ld, at::Tensor lc,
                                      at::Tensor cam, double shininess, bool two) {
         need_api();
+        check_operands("specular_directional", {&p, &n, &r}, {&ld, &lc, &cam});
         return SpecularFn::apply(p, n, r, ld, lc, cam, shininess, two);
     });
 }

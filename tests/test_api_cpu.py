@@ -138,3 +138,23 @@ def test_tensor_inputs_without_a_gpu_raise_the_same_error():
     t = [torch.zeros((1, 8, 8, 3)), torch.zeros((1, 3, 4)), torch.zeros((1, 3, 3)), torch.zeros((1, 1, 3), dtype=torch.int32)]
     with pytest.raises(RuntimeError, match="GPU"):
         dirt_amd.rasterise_batch(*t)
+
+
+def test_fused_lighting_bindings_check_their_operands():
+    """The fused lighting helpers take raw device pointers: their bindings refuse host tensors and shapes
+    the kernels do not index by (ValueError), while dirt_amd.lighting runs CPU tensors through the
+    framework ops."""
+    ext = rasterise_ops._torch_ext()
+    if ext is None:
+        pytest.skip("the C++ extension is not built")
+    z3, p3 = torch.zeros(4, 3), torch.zeros(3)
+    with pytest.raises(ValueError, match="GPU"):
+        ext.diffuse_directional(z3, z3, p3, p3, True)
+    with pytest.raises(ValueError, match="GPU"):
+        ext.specular_directional(z3, z3, z3, p3, p3, p3, 6.0, True)
+    with pytest.raises(ValueError, match="vertex_normals"):
+        ext.vertex_normals(z3, torch.zeros(2, 3, dtype=torch.int32))
+    n = torch.nn.functional.normalize(torch.randn(5, 3), dim=-1)
+    out = lighting.diffuse_directional(n, torch.ones(5, 3), torch.tensor([0., 0., -1.]), torch.ones(3))
+    ref = lighting._diffuse_directional_ops(n, torch.ones(5, 3), torch.tensor([0., 0., -1.]), torch.ones(3), True)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
