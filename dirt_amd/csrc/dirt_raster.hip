@@ -820,6 +820,7 @@ int dirt_vertex_normals_fwd(const float *vertices, int vertex_stride, const void
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     const int64_t nv = (int64_t)B * V;
     if (nv == 0) return DIRT_OK;
+    if (!vertices || !summed || !normals || (F > 0 && !faces)) return fail(DIRT_EINVAL, "vertex_normals: null pointer");
     HIP_TRY(hipMemsetAsync(summed, 0, (size_t)nv * 3 * sizeof(float), stream));
     if (F > 0 && B > 0) {
         const dim3 grid(light_blocks(F), (unsigned)B);
@@ -845,6 +846,8 @@ int dirt_vertex_normals_bwd(const float *vertices, int vertex_stride, const void
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     const int64_t nv = (int64_t)B * V;
     if (nv == 0) return DIRT_OK;
+    if (!vertices || !summed || !grad_normals || !grad_summed || !grad_vertices || (F > 0 && !faces))
+        return fail(DIRT_EINVAL, "vertex_normals: null pointer");
     HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)nv * grad_stride * sizeof(float), stream));
     if (F == 0) return DIRT_OK;
     vnormals_vertex_bwd_kernel<<<dim3(light_blocks(nv)), dim3(kLightThreads), 0, stream>>>(summed, grad_normals, nv,
@@ -866,6 +869,8 @@ int dirt_diffuse_directional_fwd(const float *normals, const float *colors, int6
 {
     if (N < 0) return fail(DIRT_EINVAL, "diffuse_directional: negative size");
     if (N == 0) return DIRT_OK;
+    if (!normals || !colors || !light_direction || !light_color || !out)
+        return fail(DIRT_EINVAL, "diffuse_directional: null pointer");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     diffuse_fwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(normals, colors, N, light_direction,
                                                                                   light_color, double_sided, out);
@@ -879,6 +884,8 @@ int dirt_diffuse_directional_bwd(const float *normals, const float *colors, int6
 {
     if (N < 0) return fail(DIRT_EINVAL, "diffuse_directional: negative size");
     if (N == 0 || (!grad_normals && !grad_colors)) return DIRT_OK;
+    if (!normals || !colors || !light_direction || !light_color || !grad_out)
+        return fail(DIRT_EINVAL, "diffuse_directional: null pointer");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     diffuse_bwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
         normals, colors, N, light_direction, light_color, double_sided, grad_out, grad_normals, grad_colors);
@@ -893,6 +900,8 @@ int dirt_specular_directional_fwd(const float *positions, const float *normals, 
 {
     if (N < 0) return fail(DIRT_EINVAL, "specular_directional: negative size");
     if (N == 0) return DIRT_OK;
+    if (!positions || !normals || !reflectivities || !light_direction || !light_color || !camera_position || !out)
+        return fail(DIRT_EINVAL, "specular_directional: null pointer");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     specular_fwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
         positions, normals, reflectivities, N, light_direction, light_color, camera_position, shininess, double_sided,
@@ -909,6 +918,8 @@ int dirt_specular_directional_bwd(const float *positions, const float *normals, 
 {
     if (N < 0) return fail(DIRT_EINVAL, "specular_directional: negative size");
     if (N == 0 || (!grad_positions && !grad_normals && !grad_reflectivities)) return DIRT_OK;
+    if (!positions || !normals || !reflectivities || !light_direction || !light_color || !camera_position || !grad_out)
+        return fail(DIRT_EINVAL, "specular_directional: null pointer");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     specular_bwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
         positions, normals, reflectivities, N, light_direction, light_color, camera_position, shininess, double_sided,

@@ -110,3 +110,15 @@ def test_recompute_backward_validates_without_a_gpu():
     assert "null" in lib.dirt_last_error().decode()
     args = [None] * 6 + [0, 16, 16, 3, 3, 1] + [None] * 4 + [0, 0, None]
     assert lib.dirt_rasterise_bwd_recompute(*args) == _lib.DIRT_OK  # B == 0: nothing to do
+
+
+def test_lighting_entry_points_reject_null_pointers_without_a_gpu():
+    """The fused lighting entry points validate sizes and pointers before touching the device (CPU-safe)."""
+    lib = _lib.load()
+    assert lib.dirt_diffuse_directional_fwd(None, None, 5, None, None, 1, None, None) == _lib.DIRT_EINVAL
+    assert lib.dirt_diffuse_directional_fwd(None, None, -1, None, None, 1, None, None) == _lib.DIRT_EINVAL
+    assert lib.dirt_specular_directional_bwd(None, None, None, 4, None, None, None, 6.0, 1, None, None, None, None,
+                                             None) == _lib.DIRT_EINVAL
+    assert lib.dirt_vertex_normals_fwd(None, 2, None, 0, 1, 3, 1, None, None, None) == _lib.DIRT_EINVAL  # stride < 3
+    assert lib.dirt_vertex_normals_fwd(None, 3, None, 0, 1, 3, 1, None, None, None) == _lib.DIRT_EINVAL  # null pointers
+    assert lib.dirt_diffuse_directional_fwd(None, None, 0, None, None, 1, None, None) == _lib.DIRT_OK  # empty
