@@ -117,7 +117,10 @@ def test_lighting_entry_points_reject_null_pointers_without_a_gpu():
     lib = _lib.load()
     assert lib.dirt_diffuse_directional_fwd(None, None, 5, None, None, 1, None, None) == _lib.DIRT_EINVAL
     assert lib.dirt_diffuse_directional_fwd(None, None, -1, None, None, 1, None, None) == _lib.DIRT_EINVAL
+    # (nothing requested: no work and no error; a requested gradient with null inputs: EINVAL before any launch)
     assert lib.dirt_specular_directional_bwd(None, None, None, 4, None, None, None, 6.0, 1, None, None, None, None,
+                                             None) == _lib.DIRT_OK
+    assert lib.dirt_specular_directional_bwd(None, None, None, 4, None, None, None, 6.0, 1, None, 16, None, None,
                                              None) == _lib.DIRT_EINVAL
     assert lib.dirt_vertex_normals_fwd(None, 2, None, 0, 1, 3, 1, None, None, None) == _lib.DIRT_EINVAL  # stride < 3
     assert lib.dirt_vertex_normals_fwd(None, 3, None, 0, 1, 3, 1, None, None, None) == _lib.DIRT_EINVAL  # null pointers
