@@ -379,6 +379,13 @@ def main():
         t_eager = timed(api_step, n_api, barrier, world, device, shared)
         g_api = graph_of(api_step, 1, cap_stream)
         t_graph = timed(g_api.replay, n_api, barrier, world, device, shared)
+        del g_api
+        # the same with 20 steps per graph (each step's fresh outputs come from the graph's pool, ~75 MB per step
+        # at c3): the replay boundary (~24 us) amortised as in the headline's 200-step graphs
+        g_api20 = graph_of(api_step, 20, cap_stream)
+        n20 = max(2, n_api // 20)
+        t_graph20 = timed(g_api20.replay, n20, barrier, world, device, shared)
+        del g_api20
         legs["api_autograd"] = {
             "what": "dirt_amd.rasterise_batch(...) + torch.autograd.grad per step (reference surface "
                     "dirt/rasterise_ops.py:57-88), fresh outputs per call, cached scratch",
@@ -386,9 +393,10 @@ def main():
             "eager_ms_per_step": round(t_eager * 1e3 / n_api, 4),
             "graph_mpix_s": round(world * B * H * W * n_api / t_graph / 1e6, 1),
             "graph_ms_per_step": round(t_graph * 1e3 / n_api, 4),
+            "graph20_mpix_s": round(world * B * H * W * n20 * 20 / t_graph20 / 1e6, 1),
+            "graph20_ms_per_step": round(t_graph20 * 1e3 / (n20 * 20), 4),
             "impl": "C++ autograd function (_dirt_torch)" if dirt_amd.rasterise_ops._torch_ext() is not None
                     else "Python torch.autograd.Function"}
-        del g_api
 
     # ---- leg: the public op surface (dirt_amd.rasterise_batch + torch.autograd), eager and graph-captured
     if not args.no_api_leg:
