@@ -60,6 +60,8 @@ SIGNATURES = {
     "dirt_vertex_normals_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
     "dirt_diffuse_directional_fwd": (_I, [_P, _P, _I64, _P, _P, _I, _P, _P]),
     "dirt_diffuse_directional_bwd": (_I, [_P, _P, _I64, _P, _P, _I, _P, _P, _P, _P]),
+    "dirt_diffuse_point_fwd": (_I, [_P, _P, _P, _I64, _P, _P, _I, _P, _P]),
+    "dirt_diffuse_point_bwd": (_I, [_P, _P, _P, _I64, _P, _P, _I, _P, _P, _P, _P, _P]),
     "dirt_specular_directional_fwd": (_I, [_P, _P, _P, _I64, _P, _P, _P, ctypes.c_float, _I, _P, _P]),
     "dirt_specular_directional_bwd": (_I, [_P, _P, _P, _I64, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _P]),
     "dirt_last_error": (ctypes.c_char_p, []),

@@ -893,6 +893,38 @@ int dirt_diffuse_directional_bwd(const float *normals, const float *colors, int6
     return DIRT_OK;
 }
 
+int dirt_diffuse_point_fwd(const float *positions, const float *normals, const float *colors, int64_t N,
+                           const float *light_position, const float *light_color, int double_sided, float *out,
+                           void *stream_)
+{
+    if (N < 0) return fail(DIRT_EINVAL, "diffuse_point: negative size");
+    if (N == 0) return DIRT_OK;
+    if (!positions || !normals || !colors || !light_position || !light_color || !out)
+        return fail(DIRT_EINVAL, "diffuse_point: null pointer");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    diffuse_point_fwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
+        positions, normals, colors, N, light_position, light_color, double_sided, out);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
+int dirt_diffuse_point_bwd(const float *positions, const float *normals, const float *colors, int64_t N,
+                           const float *light_position, const float *light_color, int double_sided,
+                           const float *grad_out, float *grad_positions, float *grad_normals, float *grad_colors,
+                           void *stream_)
+{
+    if (N < 0) return fail(DIRT_EINVAL, "diffuse_point: negative size");
+    if (N == 0 || (!grad_positions && !grad_normals && !grad_colors)) return DIRT_OK;
+    if (!positions || !normals || !colors || !light_position || !light_color || !grad_out)
+        return fail(DIRT_EINVAL, "diffuse_point: null pointer");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    diffuse_point_bwd_kernel<<<dim3(light_blocks(N)), dim3(kLightThreads), 0, stream>>>(
+        positions, normals, colors, N, light_position, light_color, double_sided, grad_out, grad_positions,
+        grad_normals, grad_colors);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
 int dirt_specular_directional_fwd(const float *positions, const float *normals, const float *reflectivities, int64_t N,
                                   const float *light_direction, const float *light_color,
                                   const float *camera_position, float shininess, int double_sided, float *out,

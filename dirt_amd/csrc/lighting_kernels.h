@@ -2,8 +2,8 @@
 // definitions (HIP_TRY, fail).  Not a standalone header.
 //
 // Fused lighting helpers of the reference's dirt/lighting.py (vertex_normals :34-98, diffuse_directional
-// :182-225, specular_directional :228-288): one kernel per forward and per backward instead of the dozen
-// elementwise launches each costs as a composition of framework ops (BASELINE config 4, the deferred-shading
+// :182-225, specular_directional :228-288, diffuse_point :291-344): one kernel per forward and per backward
+// instead of the dozen elementwise launches each costs as a composition of framework ops (BASELINE config 4, the deferred-shading
 // chain of samples/deferred.py:62-118, shades 512 x 512 pixels through them every step).  Formulas and operand
 // order follow dirt_amd/lighting.py's torch statement, which is the tests' fp32 reference for these kernels.
 // All of it is elementwise or a gather / scatter over faces: HBM- or latency-bound, no MFMA shape.
@@ -234,6 +234,48 @@ __global__ __launch_bounds__(kLightThreads) void specular_bwd_kernel(
         // r = l + 2 (n . tl) n, tl = -l: dn = 2 tl (dr . n) + 2 (n . tl) dr
         const float3 tl = mul3(l, -1.0f);
         st3(grad_normals + e * 3, add3(mul3(tl, 2.0f * dot3(dr, nv)), mul3(dr, 2.0f * dot3(nv, tl))));
+    }
+}
+
+// ---- diffuse_point (dirt/lighting.py:291-344), in dirt_amd/lighting.py's operand order:
+//   d = p - light_position,  u = d / (|d| + 1e-12),  cos = n . u,  |cos| or max(cos, 0),  out = light_color * colour * cos
+__global__ __launch_bounds__(kLightThreads) void diffuse_point_fwd_kernel(const float *__restrict__ positions,
+                                                                          const float *__restrict__ normals,
+                                                                          const float *__restrict__ colors, int64_t n,
+                                                                          const float *__restrict__ lpos,
+                                                                          const float *__restrict__ lcol, int two,
+                                                                          float *__restrict__ out)
+{
+    const int64_t e = (int64_t)blockIdx.x * kLightThreads + threadIdx.x;
+    if (e >= n) return;
+    const float3 d = sub3(ld3(positions + e * 3), ld3(lpos)), lc = ld3(lcol), col = ld3(colors + e * 3);
+    const float3 u = mul3(d, 1.0f / (norm3(d) + 1.e-12f));
+    const float cs = shade_clamp(dot3(ld3(normals + e * 3), u), two);
+    st3(out + e * 3, make_float3(lc.x * col.x * cs, lc.y * col.y * cs, lc.z * col.z * cs));
+}
+
+__global__ __launch_bounds__(kLightThreads) void diffuse_point_bwd_kernel(
+    const float *__restrict__ positions, const float *__restrict__ normals, const float *__restrict__ colors, int64_t n,
+    const float *__restrict__ lpos, const float *__restrict__ lcol, int two, const float *__restrict__ grad,
+    float *__restrict__ grad_positions, float *__restrict__ grad_normals, float *__restrict__ grad_colors)
+{
+    const int64_t e = (int64_t)blockIdx.x * kLightThreads + threadIdx.x;
+    if (e >= n) return;
+    const float3 d = sub3(ld3(positions + e * 3), ld3(lpos)), lc = ld3(lcol), col = ld3(colors + e * 3);
+    const float3 nv = ld3(normals + e * 3), g = ld3(grad + e * 3);
+    const float m = norm3(d), dm = m + 1.e-12f;
+    const float3 u = mul3(d, 1.0f / dm);
+    const float c = dot3(nv, u), cs = shade_clamp(c, two);
+    const float3 glc = make_float3(g.x * lc.x, g.y * lc.y, g.z * lc.z);
+    if (grad_colors) st3(grad_colors + e * 3, mul3(glc, cs));
+    const float dc = shade_clamp_grad(c, dot3(glc, col), two);
+    if (grad_normals) st3(grad_normals + e * 3, mul3(u, dc));
+    if (grad_positions) {
+        // u = d / (|d| + eps): dd = du / (|d| + eps) - d (d . du) / (|d| (|d| + eps)^2), du = dc n
+        const float3 du = mul3(nv, dc);
+        float3 dd = mul3(du, 1.0f / dm);
+        if (m > 0.0f) dd = sub3(dd, mul3(d, dot3(d, du) / (m * dm * dm)));
+        st3(grad_positions + e * 3, dd);
     }
 }
 

@@ -38,6 +38,8 @@ struct Api {
     decltype(&dirt_vertex_normals_bwd) vn_bwd = nullptr;
     decltype(&dirt_diffuse_directional_fwd) diffuse_fwd = nullptr;
     decltype(&dirt_diffuse_directional_bwd) diffuse_bwd = nullptr;
+    decltype(&dirt_diffuse_point_fwd) point_fwd = nullptr;
+    decltype(&dirt_diffuse_point_bwd) point_bwd = nullptr;
     decltype(&dirt_specular_directional_fwd) specular_fwd = nullptr;
     decltype(&dirt_specular_directional_bwd) specular_bwd = nullptr;
 } g_api;
@@ -71,6 +73,8 @@ void init(const std::string &path)
     g_api.vn_bwd = reinterpret_cast<decltype(g_api.vn_bwd)>(sym("dirt_vertex_normals_bwd"));
     g_api.diffuse_fwd = reinterpret_cast<decltype(g_api.diffuse_fwd)>(sym("dirt_diffuse_directional_fwd"));
     g_api.diffuse_bwd = reinterpret_cast<decltype(g_api.diffuse_bwd)>(sym("dirt_diffuse_directional_bwd"));
+    g_api.point_fwd = reinterpret_cast<decltype(g_api.point_fwd)>(sym("dirt_diffuse_point_fwd"));
+    g_api.point_bwd = reinterpret_cast<decltype(g_api.point_bwd)>(sym("dirt_diffuse_point_bwd"));
     g_api.specular_fwd = reinterpret_cast<decltype(g_api.specular_fwd)>(sym("dirt_specular_directional_fwd"));
     g_api.specular_bwd = reinterpret_cast<decltype(g_api.specular_bwd)>(sym("dirt_specular_directional_bwd"));
 }
@@ -395,6 +399,37 @@ struct DiffuseFn : public torch::autograd::Function<DiffuseFn> {
     }
 };
 
+struct DiffusePointFn : public torch::autograd::Function<DiffusePointFn> {
+    static at::Tensor forward(AutogradContext *ctx, at::Tensor positions, at::Tensor normals, at::Tensor colors,
+                              at::Tensor light_position, at::Tensor light_color, bool double_sided)
+    {
+        c10::hip::HIPGuard guard(positions.device().index());
+        at::Tensor out = at::empty_like(positions);
+        check(g_api.point_fwd(positions.data_ptr<float>(), normals.data_ptr<float>(), colors.data_ptr<float>(),
+                              positions.numel() / 3, light_position.data_ptr<float>(), light_color.data_ptr<float>(),
+                              double_sided, out.data_ptr<float>(), stream_of(positions)));
+        ctx->save_for_backward({positions, normals, colors, light_position, light_color});
+        ctx->saved_data["two"] = double_sided;
+        return out;
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list grads)
+    {
+        auto sv = ctx->get_saved_variables();
+        const at::Tensor &positions = sv[0], &normals = sv[1], &colors = sv[2];
+        c10::hip::HIPGuard guard(positions.device().index());
+        at::Tensor g = grad_or_zeros(grads[0], positions);
+        const bool wp = ctx->needs_input_grad(0), wn = ctx->needs_input_grad(1), wc = ctx->needs_input_grad(2);
+        at::Tensor gp = wp ? at::empty_like(positions) : at::Tensor(), gn = wn ? at::empty_like(normals) : at::Tensor(),
+                   gc = wc ? at::empty_like(colors) : at::Tensor();
+        check(g_api.point_bwd(positions.data_ptr<float>(), normals.data_ptr<float>(), colors.data_ptr<float>(),
+                              positions.numel() / 3, sv[3].data_ptr<float>(), sv[4].data_ptr<float>(),
+                              ctx->saved_data["two"].toBool(), g.data_ptr<float>(), wp ? gp.data_ptr<float>() : nullptr,
+                              wn ? gn.data_ptr<float>() : nullptr, wc ? gc.data_ptr<float>() : nullptr,
+                              stream_of(positions)));
+        return {gp, gn, gc, at::Tensor(), at::Tensor(), at::Tensor()};
+    }
+};
+
 struct SpecularFn : public torch::autograd::Function<SpecularFn> {
     static at::Tensor forward(AutogradContext *ctx, at::Tensor positions, at::Tensor normals, at::Tensor reflectivities,
                               at::Tensor light_direction, at::Tensor light_color, at::Tensor camera_position,
@@ -484,6 +519,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
         need_api();
         check_operands("diffuse_directional", {&n, &c}, {&ld, &lc});
         return DiffuseFn::apply(n, c, ld, lc, two);
+    });
+    m.def("diffuse_point", [](at::Tensor p, at::Tensor n, at::Tensor c, at::Tensor lp, at::Tensor lc, bool two) {
+        need_api();
+        check_operands("diffuse_point", {&p, &n, &c}, {&lp, &lc});
+        return DiffusePointFn::apply(p, n, c, lp, lc, two);
     });
     m.def("specular_directional", [](at::Tensor p, at::Tensor n, at::Tensor r, at::Tensor ld, at::Tensor lc,
                                      at::Tensor cam, double shininess, bool two) {

@@ -5,10 +5,10 @@ Gouraud (direct) shading or shade a G-buffer (deferred shading, samples/deferred
 differentiable through torch autograd, so gradients flow from pixels through the rasterise op into
 normals and geometry (BASELINE config 4: "gradient through normals").
 
-On the GPU, vertex_normals, diffuse_directional and specular_directional run as fused HIP kernels (one launch
-per forward and per backward, dirt_amd/csrc/lighting_kernels.h, C ABI dirt_vertex_normals_* /
-dirt_diffuse_directional_* / dirt_specular_directional_*) when their operands are float32 tensors on one GPU,
-of one [..., 3] shape, with light parameters of shape [3] that need no gradient and a Python-number
+On the GPU, vertex_normals, diffuse_directional, specular_directional and diffuse_point run as fused HIP
+kernels (one launch per forward and per backward, dirt_amd/csrc/lighting_kernels.h, C ABI
+dirt_vertex_normals_* / dirt_diffuse_directional_* / dirt_specular_directional_* / dirt_diffuse_point_*) when
+their operands are float32 tensors on one GPU, of one [..., 3] shape, with light parameters of shape [3] that need no gradient and a Python-number
 shininess; anything else -- CPU tensors, broadcasting, gradients with respect to the light -- runs the
 framework-op statement below (`_*_ops`), which is also the fused kernels' fp32 test reference.
 """
@@ -179,6 +179,20 @@ def diffuse_point(vertex_positions, vertex_normals, vertex_colors, light_positio
     dev, dt = vertex_positions.device, vertex_positions.dtype
     as_t = lambda x: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
     vertex_normals, vertex_colors = as_t(vertex_normals), as_t(vertex_colors)
+    if (_gpu_f32(vertex_positions, vertex_normals, vertex_colors) and vertex_positions.shape[-1:] == (3,) and
+            vertex_normals.shape == vertex_positions.shape and vertex_colors.shape == vertex_positions.shape):
+        lp, lc = _light_param(light_position, vertex_positions), _light_param(light_color, vertex_positions)
+        ext = _fused() if lp is not None and lc is not None else None
+        if ext is not None:
+            return ext.diffuse_point(vertex_positions.contiguous(), vertex_normals.contiguous(),
+                                     vertex_colors.contiguous(), lp, lc, bool(double_sided))
+    return _diffuse_point_ops(vertex_positions, vertex_normals, vertex_colors, light_position, light_color,
+                              double_sided)
+
+
+def _diffuse_point_ops(vertex_positions, vertex_normals, vertex_colors, light_position, light_color, double_sided):
+    dev, dt = vertex_positions.device, vertex_positions.dtype
+    as_t = lambda x: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
     light_position, light_color = as_t(light_position), as_t(light_color)
     rel = vertex_positions - light_position[..., None, :]
     incident = rel / (torch.linalg.norm(rel, dim=-1, keepdim=True) + 1.e-12)

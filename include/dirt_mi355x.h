@@ -73,7 +73,7 @@ extern "C" {
  * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
  * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer; 8: + dirt_rasterise_bwd_recompute,
  * dirt_bwd_recompute_workspace_size; 9: + the fused lighting helpers dirt_vertex_normals_*,
- * dirt_diffuse_directional_*, dirt_specular_directional_*) */
+ * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -190,8 +190,8 @@ int dirt_check_faces(const int32_t *faces, int B, int V, int F, void *scratch, s
 int dirt_profile_enable(int enable);
 int dirt_profile_read(int kernel_id, const char **name, int *launches, double *total_ms);
 
-/* Fused lighting helpers: dirt/lighting.py's vertex_normals (:34-98), diffuse_directional (:182-225) and
- * specular_directional (:228-288) -- TensorFlow compositions in the reference (no op of librasterise.so), one
+/* Fused lighting helpers: dirt/lighting.py's vertex_normals (:34-98), diffuse_directional (:182-225),
+ * specular_directional (:228-288) and diffuse_point (:291-344) -- TensorFlow compositions in the reference (no op of librasterise.so), one
  * kernel per forward / backward here (the deferred-shading chain of samples/deferred.py:62-118 runs them per
  * pixel).  Formulas: dirt_amd/lighting.py.  Light parameters are DEVICE pointers to 3 floats; gradients with
  * respect to them are not computed (the Python layer uses its framework-op statement when they are needed).
@@ -215,6 +215,15 @@ int dirt_diffuse_directional_fwd(const float *normals, const float *colors, int6
 int dirt_diffuse_directional_bwd(const float *normals, const float *colors, int64_t N, const float *light_direction,
                                  const float *light_color, int double_sided, const float *grad_out,
                                  float *grad_normals, float *grad_colors, void *stream);
+/* diffuse_point: positions, normals, colors, out [N,3]; out = light_color * colors * clamp(normals . unit(positions -
+ * light_position)).  Backward: grad_positions / grad_normals / grad_colors [N,3] overwritten (each may be NULL). */
+int dirt_diffuse_point_fwd(const float *positions, const float *normals, const float *colors, int64_t N,
+                           const float *light_position, const float *light_color, int double_sided, float *out,
+                           void *stream);
+int dirt_diffuse_point_bwd(const float *positions, const float *normals, const float *colors, int64_t N,
+                           const float *light_position, const float *light_color, int double_sided,
+                           const float *grad_out, float *grad_positions, float *grad_normals, float *grad_colors,
+                           void *stream);
 /* specular_directional: positions, normals, reflectivities, out [N,3]; Phong lobe around the reflected light
  * direction, out = light_color * reflectivities * clamp(cos)^shininess.  Backward: the three input gradients
  * [N,3] overwritten (each may be NULL). */

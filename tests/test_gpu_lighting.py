@@ -103,6 +103,27 @@ def test_specular_directional_fused_matches_ops(two, shininess):
         _close_grad(a, b, name)
 
 
+@pytest.mark.parametrize("two", [True, False])
+def test_diffuse_point_fused_matches_ops(two):
+    gen = torch.Generator(device=DEV).manual_seed(4)
+    N = 50003
+    p = (torch.rand((N, 3), device=DEV, generator=gen) * 2 - 1).requires_grad_(True)
+    n = torch.randn((N, 3), device=DEV, generator=gen)
+    n = (n / n.norm(dim=-1, keepdim=True)).requires_grad_(True)
+    c = torch.rand((N, 3), device=DEV, generator=gen).requires_grad_(True)
+    lp = torch.tensor([0.5, -1.0, 0.5], device=DEV)
+    lc = torch.tensor([1.0, 0.5, 0.9], device=DEV)
+    y = lighting.diffuse_point(p, n, c, lp, lc, double_sided=two)
+    _fused_node(y, "DiffusePointFn")
+    p2, n2, c2 = (t.detach().clone().requires_grad_(True) for t in (p, n, c))
+    y2 = lighting._diffuse_point_ops(p2, n2, c2, lp, lc, two)
+    torch.testing.assert_close(y, y2, rtol=1e-5, atol=2e-6)
+    g = torch.randn((N, 3), device=DEV, generator=gen)
+    for a, b, name in zip(torch.autograd.grad(y, [p, n, c], g), torch.autograd.grad(y2, [p2, n2, c2], g),
+                          ("d positions", "d normals", "d colors")):
+        _close_grad(a, b, name)
+
+
 def test_light_gradient_falls_back_to_framework_ops():
     """A light direction that needs a gradient is outside the fused kernels: the framework ops run and
     differentiate it."""
