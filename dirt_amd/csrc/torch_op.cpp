@@ -211,6 +211,9 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
                             (unsigned)fwd_flags | DIRT_FWD_SCRATCH_CLEAN, zgv, zgc, stream));
         }
         drop.armed = false;
+        // the backward takes the pixels' gradient only: without this, autograd would fill a zero gradient for
+        // each non-differentiable output (the int32 g-buffer: a 4 MB fill kernel per backward at config 3)
+        ctx->set_materialize_grads(false);
         ctx->save_for_backward({vertices, vertex_colors, faces, pixels, gbuffer, saved});
         ctx->saved_data["dims"] = std::vector<int64_t>{B, H, W, C, V, F, shader_id};
         ctx->saved_data["prezeroed"] = need_grad;

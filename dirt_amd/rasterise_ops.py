@@ -187,6 +187,8 @@ class _RasteriseFunction(torch.autograd.Function):
         ctx.shader_id = shader_id
         ctx.prezeroed = (gv, gc) if need_grad else None
         ctx.mark_non_differentiable(gbuffer, *extra)
+        # only the pixels' gradient is read: no zero gradients filled for the non-differentiable outputs
+        ctx.set_materialize_grads(False)
         return (pixels, gbuffer) + extra
 
     @staticmethod
