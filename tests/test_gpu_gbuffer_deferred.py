@@ -188,6 +188,35 @@ def test_config4_deferred_chain_matches_oracle_autograd():
     assert np.all(err <= 1e-2 * np.abs(gc) + 1e-3 * scale), "max err %g of scale %g" % (err.max(), scale)
 
 
+@pytest.mark.parametrize("seed", [2, 3, 4])
+def test_config4_chain_all_on_gpu_against_oracle_chain(seed):
+    """The whole chain on the GPU -- clip transform, the fused vertex normals and lighting kernels, the renders
+    and their backward -- against the same chain with the oracle's renders and the framework-op lighting under
+    CPU autograd (n = 50 mesh, 256^2, the surface's rows jittered per seed).  Both sides see their own float32
+    geometry (the clip transform and the normals round differently on the two devices, so a pixel whose centre
+    lies on an edge may change sides): loss within 1e-4 relative, d loss / d world vertices within 1e-2 in
+    relative L2 norm."""
+    H = W = 256
+    world, faces, albedo, wts = _chain_inputs(n=50, H=H, W=W, seed=seed)
+    world = world + np.random.default_rng(seed).normal(0.0, 0.003, world.shape).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    Vg = torch.from_numpy(world).to(dev).requires_grad_(True)
+    Lg, _, validg = dp.chain(dp.hip_render, Vg, torch.from_numpy(faces).to(dev), torch.from_numpy(albedo).to(dev),
+                             H, W, torch.from_numpy(wts).to(dev))
+    assert "VertexNormalsFn" in lighting.vertex_normals(Vg, torch.from_numpy(faces).to(dev)).grad_fn.name()
+    Lg.backward()
+    Vc = torch.from_numpy(world).requires_grad_(True)
+    Lc, _, validc = dp.chain(dp.oracle_render, Vc, torch.from_numpy(faces), torch.from_numpy(albedo), H, W,
+                             torch.from_numpy(wts))
+    Lc.backward()
+    assert abs(float(Lg.detach()) - float(Lc.detach())) <= 1e-4 * abs(float(Lc.detach()))
+    assert float((validg.cpu() != validc).float().mean()) < 1e-3
+    gg, gc = Vg.grad.cpu().numpy(), Vc.grad.numpy()
+    assert np.all(np.isfinite(gg)) and np.abs(gc).max() > 0
+    rel_l2 = float(np.linalg.norm(gg - gc) / np.linalg.norm(gc))
+    assert rel_l2 < 1e-2, rel_l2
+
+
 def test_config4_deferred_chain_finite_differences():
     """Pins the chain's gradient against central differences of the HIP forward chain on interior
     pixels (every pixel of the loss >= 3 px inside the silhouette, from face_ids): the loss is then
