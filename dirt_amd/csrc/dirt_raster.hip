@@ -449,8 +449,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
     if (B == 0) return DIRT_OK;
-    if (!pixels || !grad_pixels || !gbuffer || !saved || !grad_background ||
-        (V > 0 && (!grad_vertices || !grad_vertex_colors)))
+    if (!pixels || !grad_pixels || !gbuffer || !saved || (V > 0 && (!grad_vertices || !grad_vertex_colors)))
         return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
     Layout L;
     rc = make_layout(B, H, W, F, 0, L);
@@ -519,7 +518,7 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
     if (B == 0) return DIRT_OK;
-    if (!pixels || !grad_pixels || !grad_background || !workspace || (F > 0 && (!faces || !vertices)) ||
+    if (!pixels || !grad_pixels || !workspace || (F > 0 && (!faces || !vertices)) ||
         (V > 0 && (!grad_vertices || !grad_vertex_colors)))
         return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
     Layout L;

@@ -523,7 +523,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
 
     // ---- phase B: per-pixel contributions to the face visible at this pixel
     const int32_t rp = gp >= 0 ? (gp & kGbufIndexMask) : gp;
-    if (in_frame) {
+    if (in_frame && grad_bg != nullptr) {  // (null: the caller needs no background gradient)
         float *gbg_f = grad_bg + (int64_t)b * H * W * C;
         const uint32_t o = (uint32_t)((H - 1 - j) * W + i);
         float *gbq = gbg_f + o * (uint32_t)C;  // (RGB: one global_store_dwordx3)

@@ -255,11 +255,12 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
             gv = at::empty({B, V, 4}, f32);
             gc = at::empty({B, V, C}, f32);
         }
-        at::Tensor gbg = at::empty({B, H, W, C}, f32);
+        // (a background that needs no gradient -- a constant one -- is not written at all)
+        at::Tensor gbg = ctx->needs_input_grad(0) ? at::empty({B, H, W, C}, f32) : at::Tensor();
         check(g_api.bwd(vertices.data_ptr<float>(), vertex_colors.data_ptr<float>(), faces.data_ptr<int32_t>(),
                         pixels.data_ptr<float>(), gp.data_ptr<float>(), gbuffer.data_ptr<int32_t>(), saved.data_ptr(),
                         (int)B, (int)H, (int)W, (int)C, (int)V, (int)F, gv.data_ptr<float>(), gc.data_ptr<float>(),
-                        gbg.data_ptr<float>(), flags, stream));
+                        gbg.defined() ? gbg.data_ptr<float>() : nullptr, flags, stream));
         return {gbg, gv, gc, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
                 at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
     }

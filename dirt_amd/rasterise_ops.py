@@ -233,15 +233,17 @@ class _RasteriseFunction(torch.autograd.Function):
         else:
             grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
             grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
-        grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
+        # (a background that needs no gradient is not written at all)
+        grad_background = (torch.empty((B, H, W, C), dtype=torch.float32, device=dev) if ctx.needs_input_grad[0]
+                           else None)
         lib = _lib.load()
         with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             _lib.check(lib.dirt_rasterise_bwd(
                 vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), pixels.data_ptr(),
                 grad_pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(),
-                B, H, W, C, V, F, grad_vertices.data_ptr(), grad_colors.data_ptr(), grad_background.data_ptr(),
-                flags, stream))
+                B, H, W, C, V, F, grad_vertices.data_ptr(), grad_colors.data_ptr(),
+                grad_background.data_ptr() if grad_background is not None else None, flags, stream))
         return (grad_background, grad_vertices, grad_colors) + (None,) * 9
 
 

@@ -139,7 +139,9 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
 
 /* Backward: given grad_pixels = dL/dpixels, writes dL/dvertices [B,V,4] (z component is 0),
  * dL/dvertex_colors [B,V,C] and dL/dbackground [B,H,W,C].  All three outputs are fully
- * overwritten (see DIRT_BWD_ACCUMULATE).  Filter-based (DIRT/OpenDR) derivative, DESIGN.md section 4. */
+ * overwritten (see DIRT_BWD_ACCUMULATE).  grad_background may be NULL when the caller needs no background
+ * gradient (a constant background: 4 C bytes per pixel not written).  Filter-based (DIRT/OpenDR) derivative,
+ * DESIGN.md section 4. */
 int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces,
                        const float *pixels, const float *grad_pixels, const int32_t *gbuffer,
                        const void *saved,

@@ -671,3 +671,32 @@ def test_fused_small_scene_clipping_and_shared_mesh():
     bg, v, c, f = scenes.shared_mesh_scene(n=5)  # 2 layers x 32 faces: the first layer alone is fused
     check_scene(bg, v, c, f[:32])
     check_scene(bg, v, c, f[:33])  # one face more: the binned path, same answer as the oracle
+
+
+@pytest.mark.parametrize("impl", ["cpp", "python"])
+def test_backward_without_background_gradient(impl, monkeypatch):
+    """A background that needs no gradient (a constant one, as in samples/deferred.py's G-buffers) is not
+    written by the backward (dirt_rasterise_bwd with grad_background = NULL): the vertex and colour gradients
+    equal the full backward's and the oracle's, through the C++ op and the Python Function alike."""
+    from dirt_amd import rasterise_ops
+    if impl == "python":
+        monkeypatch.setattr(rasterise_ops, "_torch_ext", lambda: None)
+    bg, v, c, f = scenes.random_triangles(F=3000, W=160, H=96, seed=12)
+    g = np.random.default_rng(5).standard_normal(bg.shape).astype(np.float32)
+    outs = []
+    for bg_grad in (False, True):
+        bgt = _gpu(bg).requires_grad_(bg_grad)
+        vt, ct = _gpu(v).requires_grad_(True), _gpu(c).requires_grad_(True)
+        px = rasterise_ops.rasterise(bgt, vt, ct, _gpu(f))
+        ins = [bgt, vt, ct] if bg_grad else [vt, ct]
+        grads = torch.autograd.grad(px, ins, _gpu(g))
+        outs.append([t.cpu().numpy() for t in grads[-2:]])
+        if bg_grad:
+            ref_px, ref_gb, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
+            _, _, rgbg = oracle.rasterise_bwd(v[None], c[None], f[None], ref_px, g[None], ref_gb)
+            np.testing.assert_array_equal(grads[0].cpu().numpy(), rgbg[0])
+    ref_px, ref_gb, _ = oracle.rasterise_fwd(bg[None], v[None], c[None], f[None])
+    rgv, rgc, _ = oracle.rasterise_bwd(v[None], c[None], f[None], ref_px, g[None], ref_gb)
+    for gv, gc in outs:
+        assert_close_grad(gv, rgv[0], "grad_vertices", strict=True)
+        assert_close_grad(gc, rgc[0], "grad_vertex_colors", strict=True)
