@@ -449,7 +449,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
     if (B == 0) return DIRT_OK;
-    if (!pixels || !grad_pixels || !gbuffer || !saved || (V > 0 && (!grad_vertices || !grad_vertex_colors)))
+    if (!pixels || !grad_pixels || !gbuffer || !saved || (V > 0 && !grad_vertices && !grad_vertex_colors))
         return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
     Layout L;
     rc = make_layout(B, H, W, F, 0, L);
@@ -459,25 +459,40 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
     const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
     const uint8_t *covbits = reinterpret_cast<const uint8_t *>(sv + L.saved_cov);
+    // which gradients to produce: a null grad_vertices / grad_vertex_colors is not computed at all (GM bits)
+    const int gm = (grad_vertices ? 1 : 0) | (grad_vertex_colors ? 2 : 0);
     if (V > 0 && !(flags & DIRT_BWD_ACCUMULATE)) {
-        const int64_t na = (int64_t)B * V * 4, nb = (int64_t)B * V * C;
-        const int64_t blocks = std::min<int64_t>(2048, (na / 4 + 255) / 256 + 1);
+        const int64_t na = grad_vertices ? (int64_t)B * V * 4 : 0, nb = grad_vertex_colors ? (int64_t)B * V * C : 0;
+        const int64_t blocks = std::min<int64_t>(2048, (std::max(na, nb) / 4 + 255) / 256 + 1);
         zero2_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(grad_vertices, na, grad_vertex_colors, nb);
         HIP_TRY(hipGetLastError());
+    }
+    if (gm == 0) {
+        // V == 0 (no vertex or colour gradient exists): the launch still writes grad_background; the colour
+        // path's instantiation with a null colour pointer has nothing to flush (every pixel is background)
+        if (!grad_background) return DIRT_OK;
     }
     // backward tiles: kGradTileW x grad_tile_h(C) (grad_kernel.h)
     const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(C) - 1) / grad_tile_h(C);
     dim3 grid((unsigned)(gntx * gnty), (unsigned)B);
     ProfScope ps(K_GRAD, stream);
-#define LAUNCH_GRAD(CC)                                                                                       \
-    grad_kernel<CC><<<grid, dim3(GradGeom<kGradTileW, grad_tile_h(CC)>::NT), 0, stream>>>(                     \
+#define LAUNCH_GRAD_GM(CC, GMV)                                                                              \
+    grad_kernel<CC, 0, kGradTileW, grad_tile_h(CC), GMV><<<grid, dim3(GradGeom<kGradTileW, grad_tile_h(CC)>::NT), 0, \
+                                                          stream>>>(                                            \
         pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,          \
         grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H))
+#define LAUNCH_GRAD(CC)                                                                                       \
+    do {                                                                                                      \
+        if (gm == 1) LAUNCH_GRAD_GM(CC, 1);                                                                   \
+        else if (gm == 2) LAUNCH_GRAD_GM(CC, 2);                                                              \
+        else LAUNCH_GRAD_GM(CC, 3);                                                                           \
+    } while (0)
     if (C == 1) LAUNCH_GRAD(1);
     else if (C == 3) LAUNCH_GRAD(3);
     else if (C == 7) LAUNCH_GRAD(7);
     else LAUNCH_GRAD(0);
 #undef LAUNCH_GRAD
+#undef LAUNCH_GRAD_GM
     HIP_TRY(hipGetLastError());
     return DIRT_OK;
 }
@@ -519,7 +534,7 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
     if (rc) return rc;
     if (B == 0) return DIRT_OK;
     if (!pixels || !grad_pixels || !workspace || (F > 0 && (!faces || !vertices)) ||
-        (V > 0 && (!grad_vertices || !grad_vertex_colors)))
+        (V > 0 && !grad_vertices && !grad_vertex_colors))
         return fail(DIRT_EINVAL, "RasteriseGrad: null tensor pointer");
     Layout L;
     rc = make_layout(B, H, W, F, 0, L);

@@ -92,6 +92,9 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
 #define DIRT_GRAD_WAVES_C3 8  // C = 3: 64 VGPRs without spills (then 7 workgroups per CU, LDS-bound);
                               // C = 1 spills at 8, the generic paths are LDS-bound at 5
 #endif
+#ifndef DIRT_GRAD_GM1_WAVES
+#define DIRT_GRAD_GM1_WAVES 6  // C = 3, vertex gradients only: 8 waves spill 30 VGPRs, 7 spill 4, 6 none (80)
+#endif
 #ifndef DIRT_GRAD_ATTR
 #define DIRT_GRAD_ATTR
 #endif
@@ -280,9 +283,11 @@ __device__ __forceinline__ int run_start(int key, int lx)  // lx: lane index wit
 // 4 skip the whole reduction, 8 skip only the global flush, 16 skip neighbour coverage tests,
 // 32 skip the DPP run scan (every lane adds into LDS), 128 phase timestamps, 256 flush sums without
 // the global atomics
-template <int CC, int AB = 0, int TWX = kGradTileW, int TH = grad_tile_h(CC)>
+// GM: which gradients the launch produces -- bit 0 the vertices' (the pairs), bit 1 the vertex colours' (the
+// colour weights); a launch without one of them neither computes, reduces nor flushes its values.
+template <int CC, int AB = 0, int TWX = kGradTileW, int TH = grad_tile_h(CC), int GM = 3>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
-                          amdgpu_waves_per_eu(CC == 3 ? DIRT_GRAD_WAVES_C3 : DIRT_GRAD_WAVES))) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
+                          amdgpu_waves_per_eu(CC == 3 ? (GM == 1 ? DIRT_GRAD_GM1_WAVES : DIRT_GRAD_WAVES_C3) : DIRT_GRAD_WAVES))) DIRT_GRAD_ATTR void grad_kernel(const float *__restrict__ pixels, const float *__restrict__ grad_pixels,
                                                    const int32_t *__restrict__ gbuffer, const uint8_t *__restrict__ covbits,
                                                    const Rec *__restrict__ recs,
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
@@ -294,9 +299,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     constexpr int NT = GradGeom<TWX, TH>::NT, kHalo = GradGeom<TWX, TH>::HX, kHaloPix = GradGeom<TWX, TH>::PIX;
     // LDS pixel stride: float4 for RGB, two float4 for 5..8 channels (wide LDS reads)
     constexpr int CP = CM == 3 ? 4 : (CM > 4 && CM <= 8) ? 8 : CM;
-    constexpr int NVM = 9 + 3 * CM;
+    static_assert(GM >= 1 && GM <= 3, "at least one of the vertex and colour gradients");
+    constexpr int kNVV = (GM & 1) ? 9 : 0;  // vertex values per record (x, y, w of three vertices), then colours
+    constexpr int NVM = kNVV + ((GM & 2) ? 3 * CM : 0);
     const int C = CC > 0 ? CC : Cdyn;
-    const int NV = 9 + 3 * C;
+    const int NV = kNVV + ((GM & 2) ? 3 * C : 0);
 #if defined(DIRT_GRAD_LDS_PAD) && DIRT_GRAD_LDS_PAD > 0
     __shared__ volatile char occupancy_probe[DIRT_GRAD_LDS_PAD];  // experiment: caps workgroups per CU
     if (threadIdx.x == 1023) occupancy_probe[0] = 0;
@@ -603,6 +610,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
         // Pass 1 decides ownership (exact integer coverage tests) into 2-bit codes (0 skip, 1 half,
         // 2 whole); pass 2 interpolates and accumulates.  Splitting keeps the coverage tests' and the
         // accumulators' registers apart (occupancy).
+        if constexpr ((GM & 1) != 0) {
         PHASE_TS(10 + (fEp[0] == 12345.f));
         if (!(AB & 17) && __builtin_amdgcn_ballot_w64(multi) == 0) {
             // No clipped face in this wave: ownership and accumulation of the four pairs without
@@ -730,15 +738,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
                     acc[i2 * 3 + a] = (rr.basis[i2] * sub[a] + rr.basis[3 + i2] * sub[3 + a]) + rr.basis[6 + i2] * sub[6 + a];
         }
         }
+        }
         // colour weights last: keeps their registers out of the pair loop's live range
         float lam[3];
-        if (!(AB & 2) && fast_lambda(rec(), multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
+        if ((GM & 2) && !(AB & 2) && fast_lambda(rec(), multi, fEp[0] * iw0, fEp[1] * iw1, fEp[2] * iw2, lam)) {
             float Gm[CM];
 #pragma unroll
             for (int c = 0; c < CM; ++c) Gm[c] = c < C ? s_G[kme * CP + c] : 0.0f;
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                for (int c = 0; c < C; ++c) acc[9 + k * C + c] = lam[k] * Gm[c];
+                for (int c = 0; c < C; ++c) acc[(kNVV + k * C + c) < NVM ? kNVV + k * C + c : 0] = lam[k] * Gm[c];
         }
     }
     if (AB & 4) {
@@ -774,8 +783,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     }
     const int kr = dpp_shl_i<1>(key, -3);
     const bool tail = key >= 0 && ((AB & 32) || lr == 15 || kr != key);
-    float *gvb = grad_verts + (int64_t)b * V * 4;
-    float *gcb = grad_colors + (int64_t)b * V * C;
+    float *gvb = (GM & 1) ? grad_verts + (int64_t)b * V * 4 : nullptr;
+    float *gcb = (GM & 2) ? grad_colors + (int64_t)b * V * C : nullptr;
     __syncthreads();  // every read of s_G / s_I is done: the union now holds tail partials
     PHASE_TS(5);
     int q = -1;
@@ -794,8 +803,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
 #pragma unroll
             for (int v = 0; v < NVM; ++v) {
                 if (v >= NV || acc[v] == 0.0f) continue;
-                if (v < 9) atomicAdd(gvb + (int64_t)vid[v / 3] * 4 + ((v % 3) == 2 ? 3 : v % 3), acc[v]);
-                else atomicAdd(gcb + (int64_t)vid[(v - 9) / C] * C + (v - 9) % C, acc[v]);
+                if (v < kNVV) atomicAdd(gvb + (int64_t)vid[v / 3] * 4 + ((v % 3) == 2 ? 3 : v % 3), acc[v]);
+                else atomicAdd(gcb + (int64_t)vid[(v - kNVV) / C] * C + (v - kNVV) % C, acc[v]);
             }
         }
     }
@@ -813,7 +822,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     for (int e0 = 0; e0 < n; e0 += per_round) {
         const int e = e0 + (t >> 6) * rpw + wl / NV, comp_id = wl - (wl / NV) * NV;
         if (wl >= rpw * NV || e >= n) continue;
-        const int kv = comp_id < 9 ? comp_id / 3 : (comp_id - 9) / C;
+        const int kv = comp_id < kNVV ? comp_id / 3 : (comp_id - kNVV) / C;
         const int vid = T.v[kv][e];
         // the record's tails are contiguous: four reads in flight per step
         const int beg = s_lbeg[e], hi = min(beg + s_lcnt[e], kTailCap);
@@ -833,11 +842,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
             if (val == 12345.f) grad_verts[0] = val;
             continue;
         }
-        if (comp_id < 9) {
+        if (comp_id < kNVV) {
             const int c3 = comp_id % 3;
             atomicAdd(gvb + (int64_t)vid * 4 + (c3 == 2 ? 3 : c3), val);
         } else {
-            atomicAdd(gcb + (int64_t)vid * C + (comp_id - 9) % C, val);
+            atomicAdd(gcb + (int64_t)vid * C + (comp_id - kNVV) % C, val);
         }
     }
     if (AB & 128) {

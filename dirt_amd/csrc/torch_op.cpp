@@ -168,19 +168,21 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
         // forward where GradMode is visible)
         const bool need_grad = grad_possible && shader_id == DIRT_SHADER_GOURAUD && V > 0 &&
                                (ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2));
+        // which accumulators the backward fills: the vertices' and / or the colours' -- the backward computes
+        // only those (a background-only gradient still runs the kernel, with both)
+        bool want_v = need_grad && ctx->needs_input_grad(1), want_c = need_grad && ctx->needs_input_grad(2);
+        if (need_grad && !want_v && !want_c) want_v = want_c = true;
         at::Tensor gv, gc;
-        if (need_grad) {  // zero-filled by the forward in passing; the backward accumulates
-            gv = at::empty({B, V, 4}, f32);
-            gc = at::empty({B, V, C}, f32);
-        }
+        if (want_v) gv = at::empty({B, V, 4}, f32);  // zero-filled by the forward in passing; the backward accumulates
+        if (want_c) gc = at::empty({B, V, C}, f32);
         if (check_faces) {
             at::Tensor flag = at::empty({256}, at::TensorOptions().dtype(at::kByte).device(dev));
             check(g_api.check_faces(faces.data_ptr<int32_t>(), (int)B, (int)V, (int)F, flag.data_ptr(), 256, stream));
         }
         const ScratchCache::Key skey{dev.index(), reinterpret_cast<uintptr_t>(stream), B, H, W, F, bin_capacity};
         at::Tensor scratch = g_scratch.get(skey, scratch_bytes, dev, stream);
-        float *zgv = need_grad ? gv.data_ptr<float>() : nullptr;
-        float *zgc = need_grad ? gc.data_ptr<float>() : nullptr;
+        float *zgv = want_v ? gv.data_ptr<float>() : nullptr;
+        float *zgc = want_c ? gc.data_ptr<float>() : nullptr;
         variable_list out{pixels, gbuffer};
         // a failed forward may leave the cached scratch's count sets dirty: drop it
         struct DropOnThrow {
@@ -217,6 +219,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
         ctx->save_for_backward({vertices, vertex_colors, faces, pixels, gbuffer, saved});
         ctx->saved_data["dims"] = std::vector<int64_t>{B, H, W, C, V, F, shader_id};
         ctx->saved_data["prezeroed"] = need_grad;
+        ctx->saved_data["want"] = (int64_t)((want_v ? 1 : 0) | (want_c ? 2 : 0));
         if (need_grad) {
             ctx->saved_data["gv"] = gv;
             ctx->saved_data["gc"] = gc;
@@ -244,6 +247,7 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
         // .grad); a second backward of the same graph (retain_graph) starts from fresh ones
         unsigned flags = 0;
         at::Tensor gv, gc;
+        const int64_t want = ctx->saved_data["want"].toInt();
         if (ctx->saved_data["prezeroed"].toBool()) {
             gv = ctx->saved_data["gv"].toTensor();
             gc = ctx->saved_data["gc"].toTensor();
@@ -252,15 +256,16 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
             ctx->saved_data.erase("gc");
             flags = DIRT_BWD_ACCUMULATE;
         } else {
-            gv = at::empty({B, V, 4}, f32);
-            gc = at::empty({B, V, C}, f32);
+            if ((want & 1) || want == 0) gv = at::empty({B, V, 4}, f32);
+            if ((want & 2) || want == 0) gc = at::empty({B, V, C}, f32);
         }
         // (a background that needs no gradient -- a constant one -- is not written at all)
         at::Tensor gbg = ctx->needs_input_grad(0) ? at::empty({B, H, W, C}, f32) : at::Tensor();
         check(g_api.bwd(vertices.data_ptr<float>(), vertex_colors.data_ptr<float>(), faces.data_ptr<int32_t>(),
                         pixels.data_ptr<float>(), gp.data_ptr<float>(), gbuffer.data_ptr<int32_t>(), saved.data_ptr(),
-                        (int)B, (int)H, (int)W, (int)C, (int)V, (int)F, gv.data_ptr<float>(), gc.data_ptr<float>(),
-                        gbg.defined() ? gbg.data_ptr<float>() : nullptr, flags, stream));
+                        (int)B, (int)H, (int)W, (int)C, (int)V, (int)F, gv.defined() ? gv.data_ptr<float>() : nullptr,
+                        gc.defined() ? gc.data_ptr<float>() : nullptr, gbg.defined() ? gbg.data_ptr<float>() : nullptr,
+                        flags, stream));
         return {gbg, gv, gc, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(),
                 at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
     }

@@ -165,8 +165,12 @@ class _RasteriseFunction(torch.autograd.Function):
         gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
         saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
         need_grad = shader_id == _lib.SHADER_GOURAUD and any(ctx.needs_input_grad[:3]) and V > 0
-        gv = torch.empty((B, V, 4), dtype=torch.float32, device=dev) if need_grad else None
-        gc = torch.empty((B, V, C), dtype=torch.float32, device=dev) if need_grad else None
+        # the accumulators the backward fills (it computes only those; background-only: both)
+        want_v, want_c = need_grad and ctx.needs_input_grad[1], need_grad and ctx.needs_input_grad[2]
+        if need_grad and not (want_v or want_c):
+            want_v = want_c = True
+        gv = torch.empty((B, V, 4), dtype=torch.float32, device=dev) if want_v else None
+        gc = torch.empty((B, V, C), dtype=torch.float32, device=dev) if want_c else None
         with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             if check_faces:
@@ -174,7 +178,7 @@ class _RasteriseFunction(torch.autograd.Function):
             layout = (B, H, W, F, bin_capacity)
             scratch = _workspace.scratch(dev, stream, layout, scratch_bytes)
             cam = camera_pos.data_ptr() if camera_pos is not None else None
-            zg = (gv.data_ptr(), gc.data_ptr()) if need_grad else (None, None)
+            zg = (gv.data_ptr() if want_v else None, gc.data_ptr() if want_c else None)
             try:
                 extra = _RasteriseFunction._launch(lib, want_gbuf, background, vertices, vertex_colors, faces, cam,
                                                    B, H, W, C, V, F, shader_id, pixels, gbuffer, saved, saved_bytes,
@@ -186,6 +190,7 @@ class _RasteriseFunction(torch.autograd.Function):
         ctx.dims = (B, H, W, C, V, F)
         ctx.shader_id = shader_id
         ctx.prezeroed = (gv, gc) if need_grad else None
+        ctx.want = (want_v, want_c) if need_grad else (True, True)
         ctx.mark_non_differentiable(gbuffer, *extra)
         # only the pixels' gradient is read: no zero gradients filled for the non-differentiable outputs
         ctx.set_materialize_grads(False)
@@ -231,8 +236,9 @@ class _RasteriseFunction(torch.autograd.Function):
             ctx.prezeroed = None
             flags = _lib.BWD_ACCUMULATE
         else:
-            grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
-            grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
+            want_v, want_c = ctx.want
+            grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev) if want_v else None
+            grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev) if want_c else None
         # (a background that needs no gradient is not written at all)
         grad_background = (torch.empty((B, H, W, C), dtype=torch.float32, device=dev) if ctx.needs_input_grad[0]
                            else None)
@@ -242,7 +248,8 @@ class _RasteriseFunction(torch.autograd.Function):
             _lib.check(lib.dirt_rasterise_bwd(
                 vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), pixels.data_ptr(),
                 grad_pixels.data_ptr(), gbuffer.data_ptr(), saved.data_ptr(),
-                B, H, W, C, V, F, grad_vertices.data_ptr(), grad_colors.data_ptr(),
+                B, H, W, C, V, F, grad_vertices.data_ptr() if grad_vertices is not None else None,
+                grad_colors.data_ptr() if grad_colors is not None else None,
                 grad_background.data_ptr() if grad_background is not None else None, flags, stream))
         return (grad_background, grad_vertices, grad_colors) + (None,) * 9
 

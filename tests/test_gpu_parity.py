@@ -700,3 +700,51 @@ def test_backward_without_background_gradient(impl, monkeypatch):
     for gv, gc in outs:
         assert_close_grad(gv, rgv[0], "grad_vertices", strict=True)
         assert_close_grad(gc, rgc[0], "grad_vertex_colors", strict=True)
+
+
+@pytest.mark.parametrize("scene", ["c3_small", "clipping_c7", "fuzz_c5"])
+def test_backward_partial_gradients(scene):
+    """dirt_rasterise_bwd computes only the gradients it is given buffers for (grad_vertices or
+    grad_vertex_colors NULL: the other part is neither computed, reduced nor flushed): each part equals the full
+    backward's and the oracle's; the public op does the same when only vertices or only colours need a gradient."""
+    from dirt_amd import _lib, rasterise_ops
+    from dirt_amd.session import RasteriseSession
+    if scene == "c3_small":
+        bg, v, c, f = (a[None] for a in scenes.random_triangles(F=4000, W=192, H=128, seed=13))
+    elif scene == "clipping_c7":
+        bg, v, c, f = (a[None] for a in scenes.clipping_scene(C=7))
+    else:
+        bg, v, c, f = scenes.fuzz_case(9003)
+    B, H, W, C = bg.shape
+    V, F = v.shape[1], f.shape[1]
+    g = np.random.default_rng(6).standard_normal(bg.shape).astype(np.float32)
+    ref_px, ref_gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+    rgv, rgc, rgbg = oracle.rasterise_bwd(v, c, f, ref_px, g, ref_gb)
+    sess = RasteriseSession(B, H, W, C, V, F, device="cuda")
+    t = [_gpu(a) for a in (bg, v, c, f)]
+    sess.forward(*t)
+    lib = _lib.load()
+    stream = torch.cuda.current_stream().cuda_stream
+    gt = _gpu(g)
+    for want_v, want_c in ((True, False), (False, True)):
+        gv = torch.full((B, V, 4), 7.0, device="cuda") if want_v else None
+        gc = torch.full((B, V, C), 7.0, device="cuda") if want_c else None
+        gbg = torch.empty((B, H, W, C), device="cuda")
+        _lib.check(lib.dirt_rasterise_bwd(t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), sess.pixels.data_ptr(),
+                                          gt.data_ptr(), sess.gbuffer.data_ptr(), sess.saved.data_ptr(), B, H, W, C,
+                                          V, F, gv.data_ptr() if want_v else None, gc.data_ptr() if want_c else None,
+                                          gbg.data_ptr(), 0, stream))
+        np.testing.assert_array_equal(gbg.cpu().numpy(), rgbg)
+        if want_v:
+            assert_close_grad(gv.cpu().numpy(), rgv, "grad_vertices", strict=True)
+        if want_c:
+            assert_close_grad(gc.cpu().numpy(), rgc, "grad_vertex_colors", strict=True)
+    # the public op with only one of them requiring a gradient
+    for want_v in (True, False):
+        vt, ct = _gpu(v).requires_grad_(want_v), _gpu(c).requires_grad_(not want_v)
+        px = rasterise_ops.rasterise_batch(t[0], vt, ct, t[3])
+        gr, = torch.autograd.grad(px, [vt if want_v else ct], gt)
+        if want_v:
+            assert_close_grad(gr.cpu().numpy(), rgv, "grad_vertices", strict=True)
+        else:
+            assert_close_grad(gr.cpu().numpy(), rgc, "grad_vertex_colors", strict=True)
