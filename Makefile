@@ -13,8 +13,14 @@ CC ?= gcc
 # with 16.59 / 16.49 / 16.40 Gpixels/s (+2.8 %).  `make WAVEPRIO=` builds without it.
 # -Wno-pass-failed: the generic-C backward paths ask for 6 waves / SIMD although LDS caps them at 5
 WAVEPRIO ?= -mllvm -amdgpu-set-wave-priority
+# -fno-slp-vectorize: the SLP vectoriser packs pairs of fp32 operations into v_pk_* instructions whose operands
+# need even-aligned register pairs; in the backward that costs registers the 64-VGPR / 8-wave budget does not
+# have (the vertex-only instantiation spilled 30 VGPRs).  Without it, A/B in one call, three rounds
+# (profiles/r04/ab_no_slp/): c3 18.06-18.25 -> 18.28-18.50, c4 7.33-7.47 -> 7.82-7.91, c5 28.17-28.26 ->
+# 28.44-28.70 Gpixels/s (bench_configs, 10-step graphs).  `make SLP=` builds with it.
+SLP ?= -fno-slp-vectorize
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-           -fhip-fp32-correctly-rounded-divide-sqrt $(WAVEPRIO) -Wall -Wno-unused-function -Wno-pass-failed
+           -fhip-fp32-correctly-rounded-divide-sqrt $(WAVEPRIO) $(SLP) -Wall -Wno-unused-function -Wno-pass-failed
 ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall
 
 LIB = dirt_amd/libdirt_mi355x.so

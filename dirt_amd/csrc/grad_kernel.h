@@ -93,7 +93,7 @@ __device__ __forceinline__ bool fast_lambda(const Rec &r, bool multi, float a0, 
                               // C = 1 spills at 8, the generic paths are LDS-bound at 5
 #endif
 #ifndef DIRT_GRAD_GM1_WAVES
-#define DIRT_GRAD_GM1_WAVES 6  // C = 3, vertex gradients only: 8 waves spill 30 VGPRs, 7 spill 4, 6 none (80)
+#define DIRT_GRAD_GM1_WAVES 8  // C = 3, vertex gradients only (64 VGPRs without SLP vectorisation, Makefile)
 #endif
 #ifndef DIRT_GRAD_ATTR
 #define DIRT_GRAD_ATTR
