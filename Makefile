@@ -19,14 +19,18 @@ WAVEPRIO ?= -mllvm -amdgpu-set-wave-priority
 # (profiles/r04/ab_no_slp/): c3 18.06-18.25 -> 18.28-18.50, c4 7.33-7.47 -> 7.82-7.91, c5 28.17-28.26 ->
 # 28.44-28.70 Gpixels/s (bench_configs, 10-step graphs).  `make SLP=` builds with it.
 SLP ?= -fno-slp-vectorize
+# SCHED: extra scheduler options for A/B builds (`make variant NAME=x SCHED=...`).  -amdgpu-use-amdgpu-trackers
+# measured within noise over two calls (profiles/r04/ab_sched/), so the product builds without any.
+SCHED ?=
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-           -fhip-fp32-correctly-rounded-divide-sqrt $(WAVEPRIO) $(SLP) -Wall -Wno-unused-function -Wno-pass-failed
+           -fhip-fp32-correctly-rounded-divide-sqrt $(WAVEPRIO) $(SLP) $(SCHED) -Wall -Wno-unused-function \
+           -Wno-pass-failed
 ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall
 
 LIB = dirt_amd/libdirt_mi355x.so
 ORACLE = oracle/libdirt_oracle.so
 HIP_SRC = dirt_amd/csrc/dirt_raster.hip
-HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/lighting_kernels.h dirt_amd/csrc/setup_kernel.h dirt_amd/csrc/raster_kernel.h dirt_amd/csrc/grad_kernel.h dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h
+HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/lighting_kernels.h dirt_amd/csrc/setup_kernel.h dirt_amd/csrc/raster_kernel.h dirt_amd/csrc/grad_kernel.h dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h Makefile
 
 # the public op's C++ autograd function (PyTorch extension over the C ABI; dirt_amd/csrc/torch_op.cpp)
 PY ?= python3
