@@ -431,6 +431,10 @@ __device__ __forceinline__ void wave_lds_sync()
 // 20k faces, 79 workgroups) leaves most CUs idle, and 128-face workgroups there shorten the setup (c4 setup
 // 8.6-10.0 -> 7.6-8.0 us; c3, 196 workgroups, loses 1 us with them: profiles/r03/ab_setup_threads/).
 constexpr int64_t kSetupSmallGrid = 128;
+#ifndef DIRT_SETUP_SMALL_THREADS
+#define DIRT_SETUP_SMALL_THREADS (kBinThreads / 2)
+#endif
+constexpr int kSetupSmallThreads = DIRT_SETUP_SMALL_THREADS;
 
 // launch the setup (and binning) of B frames x F faces
 template <int AB = 0>
@@ -439,7 +443,7 @@ void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int
                   float *zero_a = nullptr, int64_t nzero_a = 0, float *zero_b = nullptr, int64_t nzero_b = 0)
 {
     const bool small = (int64_t)B * ((F + kBinThreads - 1) / kBinThreads) < kSetupSmallGrid;
-    const int nt = small ? kBinThreads / 2 : kBinThreads;
+    const int nt = small ? kSetupSmallThreads : kBinThreads;
     ZeroFill zf{zero_a, zero_b, zero_a ? nzero_a : 0, zero_b ? nzero_b : 0, (F + nt - 1) / nt};
     // filler workgroups per frame row: ~16 float4 stores per thread, at most 64 in all
     // (rounded up: a few accumulator floats in all, fewer than one float4, still need a filler workgroup)
@@ -448,7 +452,7 @@ void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int
     const dim3 grid((unsigned)(zf.nfb + nzb), (unsigned)B);
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
     if (small)
-        setup_kernel<AB, kBinThreads / 2><<<grid, dim3(kBinThreads / 2), 0, stream>>>(
+        setup_kernel<AB, kSetupSmallThreads><<<grid, dim3(kSetupSmallThreads), 0, stream>>>(
             vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins, L.slab, B,
             zf, gx, gy);
     else
