@@ -111,8 +111,18 @@ __device__ __forceinline__ void store_record_fast(Rec *dst, const Rec &r)
     for (int k = 0; k < 4; ++k) d4[k] = s4[k];
 }
 
+// R5 sub-vertex clamp: x/w of a clipped face's sub-vertex to [-2 gx, 2 gx] (NaN to 2 gx), y/w likewise.
+// R5's guard planes keep a sub-vertex inside the guard band only up to float rounding, and near w = 0 that
+// rounding is unbounded (an intersection computed after the x planes can land at x / w = -4.7e6 with w = 7e-12,
+// fuzz seed 167059); clamped at twice the band, which ordinary rounding never reaches, every snapped
+// coordinate stays below 2^24 (W, H <= 8192), so A, B and the offsets to X0, Y0 stay exact in int32.
+__device__ __forceinline__ float guard_clamp(float xn, float g) { return xn <= g ? (xn >= -g ? xn : -g) : g; }
+
 // R1..R4 for one (sub-)triangle: fills `out` (a register-resident local), returns true if non-empty.
-__device__ inline bool make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, Rec &out)
+// Clamp: a clipped face's sub-triangle (R5 sub-vertex clamp to gx2, gy2 = twice the guard band).
+template <bool Clamp = false>
+__device__ inline bool make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, Rec &out,
+                                   float gx2 = 0.0f, float gy2 = 0.0f)
 {
     const float hw = 0.5f * (float)W, hh = 0.5f * (float)H;
     int32_t X[3], Y[3];
@@ -121,13 +131,18 @@ __device__ inline bool make_record(const float v[3][4], const float basis[3][3],
     for (int k = 0; k < 3; ++k) {
         float iw = 1.0f / v[k][3];
         float xn = v[k][0] * iw, yn = v[k][1] * iw, zn = v[k][2] * iw;
+        if (Clamp) {
+            xn = guard_clamp(xn, gx2);
+            yn = guard_clamp(yn, gy2);
+        }
         float xw = (xn + 1.0f) * hw, yw = (yn + 1.0f) * hh;
         zw[k] = zn * 0.5f + 0.5f;
         X[k] = (int32_t)__builtin_rintf(xw * 256.0f);
         Y[k] = (int32_t)__builtin_rintf(yw * 256.0f);
         iwv[k] = iw;
     }
-    // |X|, |Y| < 2^23 (guard band 16384 px beyond the frame centre, 256 sub-pixels): A, B < 2^24 fit int32
+    // |X|, |Y| < 2^24 (the guard band is 16384 px beyond the frame centre, twice that for a clamped sub-vertex;
+    // 256 sub-pixels per pixel, W, H <= 8192): A, B < 2^25 fit int32
     // and every product is one 32 x 32 -> 64-bit multiply-add (no 64 x 64 multiplies)
     int32_t A[3], B[3];
 #pragma unroll

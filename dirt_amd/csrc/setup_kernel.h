@@ -64,7 +64,7 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
             for (int i = 0; i < 3; ++i) sb[k][i] = poly[idx[k]][4 + i];
         }
         Rec r;
-        make_record(sv, sb, W, H, f, r);
+        make_record<true>(sv, sb, W, H, f, r, 2.0f * gx, 2.0f * gy);
         frame_recs[rec_index(F, f, s)] = r;
     }
     return nsub;

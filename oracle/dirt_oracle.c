@@ -73,7 +73,14 @@ static int64_t floor_div256(int64_t v) { return v >= 0 ? v / 256 : -((-v + 255) 
 
 /* R1-R4 for one (sub-)triangle given clip coords (x,y,z,w) of three vertices and their parent basis.
  * Returns 1 if the triangle produces a non-empty record. */
-static int make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, orc_rec *r)
+/* R5 sub-vertex clamp: a clipped face's sub-vertex x/w is clamped to [-2 gx, 2 gx] (NaN to
+ * 2 gx), y/w likewise -- Sutherland-Hodgman keeps them inside the guard band only up to rounding, which near
+ * w = 0 is unbounded; ordinary rounding never reaches twice the band, and the snapped integers stay below 2^24. */
+static float guard_clamp(float xn, float g) { return xn <= g ? (xn >= -g ? xn : -g) : g; }
+
+/* clamp_g: NULL on the fast path; twice the guard band (2 gx, 2 gy) for a clipped face's sub-triangles */
+static int make_record(const float v[3][4], const float basis[3][3], int W, int H, int face, orc_rec *r,
+                       const float *clamp_g)
 {
     const float hw = 0.5f * (float)W, hh = 0.5f * (float)H;
     int32_t X[3], Y[3];
@@ -81,6 +88,10 @@ static int make_record(const float v[3][4], const float basis[3][3], int W, int 
     for (int k = 0; k < 3; ++k) {
         float iw = 1.0f / v[k][3];
         float xn = v[k][0] * iw, yn = v[k][1] * iw, zn = v[k][2] * iw;
+        if (clamp_g) {
+            xn = guard_clamp(xn, clamp_g[0]);
+            yn = guard_clamp(yn, clamp_g[1]);
+        }
         float xw = (xn + 1.0f) * hw, yw = (yn + 1.0f) * hh;
         zw[k] = zn * 0.5f + 0.5f;
         X[k] = (int32_t)rintf(xw * 256.0f);
@@ -166,7 +177,7 @@ static int setup_face(const float *verts, const int32_t *face3, int V, int W, in
     }
     if (fast) {
         const float id[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
-        make_record((const float(*)[4])v, id, W, H, f, &recs[0]);
+        make_record((const float(*)[4])v, id, W, H, f, &recs[0], NULL);
         return 1;
     }
     /* R5: Sutherland-Hodgman against near + 4 guard planes, carrying the parent basis */
@@ -204,7 +215,8 @@ static int setup_face(const float *verts, const int32_t *face3, int V, int W, in
             for (int c = 0; c < 4; ++c) sv[k][c] = poly[idx[k]][c];
             for (int i = 0; i < 3; ++i) sb[k][i] = poly[idx[k]][4 + i];
         }
-        make_record((const float(*)[4])sv, (const float(*)[3])sb, W, H, f, &recs[s]);
+        const float g2[2] = {2.0f * gx, 2.0f * gy};
+        make_record((const float(*)[4])sv, (const float(*)[3])sb, W, H, f, &recs[s], g2);
     }
     return nsub;
 }

@@ -30,13 +30,23 @@ GBUF_MULTI = 1 << 30
 EXTRA_PER_FACE = 5
 
 
-def _snap(v4, W, H):
-    """R1 + R2 in float32: snapped window coordinates (1/256 px) of one clip-space vertex."""
+def _guard_clamp(xn, g):
+    """R5 sub-vertex clamp: x/w of a clipped face's sub-vertex to [-g, g], NaN to g, g = twice the guard band
+    (DESIGN.md 3, R5)."""
+    return xn if xn <= g and xn >= -g else (-g if xn <= g else g)
+
+
+def _snap(v4, W, H, clamp=None):
+    """R1 + R2 in float32: snapped window coordinates (1/256 px) of one clip-space vertex (clamp: (2 gx, 2 gy)
+    for a clipped face's sub-vertex)."""
     x, y, w = F32(v4[0]), F32(v4[1]), F32(v4[3])
     iw = F32(1.0) / w
     hw, hh = F32(0.5) * F32(W), F32(0.5) * F32(H)
-    X = int(np.rint(((x * iw + F32(1.0)) * hw) * F32(256.0)))
-    Y = int(np.rint(((y * iw + F32(1.0)) * hh) * F32(256.0)))
+    xn, yn = x * iw, y * iw
+    if clamp is not None:
+        xn, yn = _guard_clamp(xn, clamp[0]), _guard_clamp(yn, clamp[1])
+    X = int(np.rint(((xn + F32(1.0)) * hw) * F32(256.0)))
+    Y = int(np.rint(((yn + F32(1.0)) * hh) * F32(256.0)))
     return X, Y
 
 
@@ -44,8 +54,8 @@ class Tri:
     """One rasterised (sub-)triangle: integer edge functions E_k(P) = A_k Px + B_k Py + C_k (interior
     positive, P in 1/256 px), its vertices' clip w and their parent barycentric basis."""
 
-    def __init__(self, verts7, W, H):
-        X, Y = zip(*(_snap(p[:4], W, H) for p in verts7))
+    def __init__(self, verts7, W, H, clamp=None):
+        X, Y = zip(*(_snap(p[:4], W, H, clamp) for p in verts7))
         A, B, C = [], [], []
         for k in range(3):
             a, b = (k + 1) % 3, (k + 2) % 3
@@ -120,7 +130,7 @@ def setup_face(verts, face, V, W, H):
     tris = []
     for s in range(len(poly) - 2):
         t3 = [poly[0], poly[s + 1], poly[s + 2]]
-        tri = Tri(t3, W, H)
+        tri = Tri(t3, W, H, (F32(2.0) * gx, F32(2.0) * gy))
         tris.append(tri if tri.D != 0 else None)
     return tris, True
 

@@ -59,6 +59,19 @@ def test_f64_pin_fuzz_seed_37851():
     assert ((gb >= 0) & ((gb & (1 << 30)) != 0)).any()  # clipped faces are visible
 
 
+def test_f64_pin_sub_vertex_beyond_guard_band():
+    """Fuzz seed 167059 (batch of two 33x17 frames, 5 channels): clipping faces 71 and 115 of frame 0 leaves a
+    sub-vertex at x/w = -4.7e6 (w = 7e-12), far outside the guard band; R5's sub-vertex clamp (twice the band)
+    keeps its snapped coordinates, and so every edge coefficient, inside the integer ranges both sides assume."""
+    bg, v, c, f = scenes.fuzz_case(167059)
+    B, H, W, C = bg.shape
+    for fi in (71, 115):
+        tris, clipped = backward_f64.setup_face(v[0], f[0][fi], v.shape[1], W, H)
+        assert clipped and len(tris) == 3
+        assert all(abs(x) < 2 ** 25 for t in tris if t is not None for x in t.A + t.B)
+    check_pin(bg, v, c, f, 167059)
+
+
 @pytest.mark.parametrize("block", range(5))
 def test_f64_pin_clipped_slivers(block):
     """50 scenes of guard-band and near-plane clipped slivers (10 per case)."""

@@ -443,6 +443,13 @@ def test_fuzz_adversarial_scenes(seed):
     check_scene(*scenes.fuzz_case(seed), seed=seed)
 
 
+def test_clipped_sub_vertex_beyond_guard_band():
+    """Fuzz seed 167059: clipping near w = 0 leaves a sub-vertex at x/w = -4.7e6 (the guard band is +-993 at
+    W = 33); without R5's sub-vertex clamp its snapped x overflowed int32 and the GPU and the oracle chose
+    different faces at two pixels.  Bit-exact forward, backward within tolerance."""
+    check_scene(*scenes.fuzz_case(167059), seed=167059)
+
+
 def test_extreme_w_and_constant_depth_faces():
     """Setup's division shortcuts fall back to plain IEEE division outside 2^-60 <= |x| <= 2^60 and for zero
     numerators: faces whose clip coordinates are scaled by 1e-20 / 1e20 (same projection, w outside the
@@ -707,14 +714,28 @@ def test_backward_partial_gradients(scene):
     """dirt_rasterise_bwd computes only the gradients it is given buffers for (grad_vertices or
     grad_vertex_colors NULL: the other part is neither computed, reduced nor flushed): each part equals the full
     backward's and the oracle's; the public op does the same when only vertices or only colours need a gradient."""
-    from dirt_amd import _lib, rasterise_ops
-    from dirt_amd.session import RasteriseSession
     if scene == "c3_small":
         bg, v, c, f = (a[None] for a in scenes.random_triangles(F=4000, W=192, H=128, seed=13))
     elif scene == "clipping_c7":
         bg, v, c, f = (a[None] for a in scenes.clipping_scene(C=7))
     else:
         bg, v, c, f = scenes.fuzz_case(9003)
+    _check_partial_gradients(bg, v, c, f, public_op=True, strict=True)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_GM_FUZZ_FIRST", "20000")),
+                                       int(os.environ.get("DIRT_GM_FUZZ_SEEDS", "20006"))))
+def test_backward_partial_gradients_fuzz(seed):
+    """The partial-gradient backward (vertices only, colours only) on adversarial fuzz scenes (scenes.fuzz_case:
+    slivers, clipping, guard-band overflow, 1..8 channels).  DIRT_GM_FUZZ_FIRST / DIRT_GM_FUZZ_SEEDS set the seed
+    range (default 6 seeds)."""
+    _check_partial_gradients(*scenes.fuzz_case(seed), public_op=False, strict=False)
+
+
+def _check_partial_gradients(bg, v, c, f, public_op, strict):
+    """(strict: the tight contract of the golden and full-size scenes; fuzz scenes use the suite's default)"""
+    from dirt_amd import _lib, rasterise_ops
+    from dirt_amd.session import RasteriseSession
     B, H, W, C = bg.shape
     V, F = v.shape[1], f.shape[1]
     g = np.random.default_rng(6).standard_normal(bg.shape).astype(np.float32)
@@ -736,15 +757,15 @@ def test_backward_partial_gradients(scene):
                                           gbg.data_ptr(), 0, stream))
         np.testing.assert_array_equal(gbg.cpu().numpy(), rgbg)
         if want_v:
-            assert_close_grad(gv.cpu().numpy(), rgv, "grad_vertices", strict=True)
+            assert_close_grad(gv.cpu().numpy(), rgv, "grad_vertices", strict=strict)
         if want_c:
-            assert_close_grad(gc.cpu().numpy(), rgc, "grad_vertex_colors", strict=True)
+            assert_close_grad(gc.cpu().numpy(), rgc, "grad_vertex_colors", strict=strict)
     # the public op with only one of them requiring a gradient
-    for want_v in (True, False):
+    for want_v in ((True, False) if public_op else ()):
         vt, ct = _gpu(v).requires_grad_(want_v), _gpu(c).requires_grad_(not want_v)
         px = rasterise_ops.rasterise_batch(t[0], vt, ct, t[3])
         gr, = torch.autograd.grad(px, [vt if want_v else ct], gt)
         if want_v:
-            assert_close_grad(gr.cpu().numpy(), rgv, "grad_vertices", strict=True)
+            assert_close_grad(gr.cpu().numpy(), rgv, "grad_vertices", strict=strict)
         else:
-            assert_close_grad(gr.cpu().numpy(), rgc, "grad_vertex_colors", strict=True)
+            assert_close_grad(gr.cpu().numpy(), rgc, "grad_vertex_colors", strict=strict)
