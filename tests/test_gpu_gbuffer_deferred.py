@@ -56,11 +56,13 @@ def test_gbuffer_outputs_bit_exact(name):
     assert np.abs(bary[cov].sum(-1) - 1.0).max() < 1e-5
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_GBUF_FUZZ_SEEDS", "12"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_GBUF_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_GBUF_FUZZ_SEEDS", "12"))))
 def test_gbuffer_outputs_adversarial_fuzz(seed):
     """The G-buffer instantiation of the raster (depth, barycentrics, face ids) on the adversarial fuzz scenes
     of tests/test_gpu_parity.py (pixel-centre vertices, slivers, ties, clipping, w <= 0, guard-band overflow),
-    bit-exact against the oracle.  DIRT_GBUF_FUZZ_SEEDS=N widens it (default 12)."""
+    bit-exact against the oracle.  DIRT_GBUF_FUZZ_SEEDS=N widens it to the seeds below N (default 12),
+    from DIRT_GBUF_FUZZ_FIRST."""
     W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
     C = (3, 7, 1, 5)[seed % 4]
     _gbuffer_scene(*scenes.adversarial_scene(100000 + seed, W=W, H=H, C=C))

@@ -213,11 +213,13 @@ def test_hill_overlap_and_mesh():
     np.testing.assert_array_equal(px, rpx)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_PROC_FUZZ_SEEDS", "6"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_PROC_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_PROC_FUZZ_SEEDS", "6"))))
 def test_procedural_programs_adversarial_fuzz(seed):
     """The depth-tested procedural programs (oceanic_horizon and the oceanic family, shader ids 1..6 in turn)
     on the adversarial fuzz scenes (pixel-centre vertices, slivers, depth ties, clipping, w <= 0): bit-exact
-    g-buffer and pixels.  DIRT_PROC_FUZZ_SEEDS=N widens it (default 6: each program once)."""
+    g-buffer and pixels.  DIRT_PROC_FUZZ_SEEDS=N widens it to the seeds below N (default 6: each program once),
+    from DIRT_PROC_FUZZ_FIRST."""
     W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
     sid = 1 + seed % 6
     bg, v, c, f = (a[None] for a in scenes.adversarial_scene(300000 + seed, W=W, H=H, C=3))
@@ -228,11 +230,13 @@ def test_procedural_programs_adversarial_fuzz(seed):
     np.testing.assert_array_equal(px, rpx)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_HILL_FUZZ_SEEDS", "8"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_HILL_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_HILL_FUZZ_SEEDS", "8"))))
 def test_hill_adversarial_fuzz(seed):
     """hill (no depth test: the last face in draw order wins) on the adversarial fuzz scenes of
     tests/test_gpu_parity.py -- pixel-centre vertices, slivers, duplicates, clipping, w <= 0 -- bit-exact
-    g-buffer and pixels.  DIRT_HILL_FUZZ_SEEDS=N widens it (default 8)."""
+    g-buffer and pixels.  DIRT_HILL_FUZZ_SEEDS=N widens it to the seeds below N (default 8),
+    from DIRT_HILL_FUZZ_FIRST."""
     W, H = [(64, 48), (33, 17), (130, 70)][seed % 3]
     _, v, _, f = scenes.adversarial_scene(200000 + seed, W=W, H=H, C=3)
     T = scenes.hill_terrain(H, W, 4)[None]

@@ -643,13 +643,15 @@ def test_dense_tiles_with_clipped_faces(C):
     check_scene(bg, v, c, f)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUSED_FUZZ_SEEDS", "24"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUSED_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_FUSED_FUZZ_SEEDS", "24"))))
 def test_fused_small_scene_forward(seed):
     """Frames of at most 32 faces take the fused forward (raster_kernel FUSED: each workgroup sets up the
     frame's faces in LDS, no setup launch, no bins; tile 0 publishes the records for the backward).
     Adversarial small scenes (clipping, ties, slivers, w <= 0), batches and channel counts: bit-exact
     forward, gradients in tolerance -- the backward reads the records the fused forward published.
-    DIRT_FUSED_FUZZ_SEEDS=N widens it (default 24)."""
+    DIRT_FUSED_FUZZ_SEEDS=N widens it to the seeds below N (default 24),
+    from DIRT_FUSED_FUZZ_FIRST."""
     W, H = [(64, 48), (33, 17), (130, 70), (16, 16)][seed % 4]
     C = (3, 1, 7, 5)[seed % 4]
     if seed % 3 == 2:
