@@ -20,12 +20,16 @@ __device__ inline float plane_dist(int p, const float *v, float gx, float gy)
     }
 }
 
+// a triangle clipped by 5 planes has at most 8 vertices (6 fan sub-triangles: kExtraPerFace + 1)
+constexpr int kMaxClipVerts = 8;
+static_assert(kMaxClipVerts - 2 == kExtraPerFace + 1, "sub-triangle slots");
+
 // R5 slow path: clip against z>=-w and the guard planes, fan-triangulate, write the sub-records.
 // Not inlined so that its stack arrays do not inflate the fast path.  Returns nsub.
 __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *frame_recs)
 {
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
-    float poly[9][7], tmp[9][7];
+    float poly[kMaxClipVerts][7], tmp[kMaxClipVerts][7];
     int n = 3;
     for (int k = 0; k < 3; ++k) {
         for (int c = 0; c < 4; ++c) poly[k][c] = tri.v[k][c];
@@ -38,6 +42,9 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
             const float *c = poly[(i + 1) % n];
             const float da = plane_dist(p, a, gx, gy), dc = plane_dist(p, c, gx, gy);
             const bool ina = da >= 0.0f, inc = dc >= 0.0f;
+            // R5 vertex cap: more than 8 vertices (possible only when rounding near w = 0 makes the polygon
+            // non-convex) culls the face -- it would need more than the 6 sub-triangle slots
+            if ((ina ? 1 : 0) + (ina != inc ? 1 : 0) > kMaxClipVerts - m) return 0;
             if (ina) {
                 for (int q = 0; q < 7; ++q) tmp[m][q] = a[q];
                 ++m;

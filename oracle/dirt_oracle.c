@@ -194,6 +194,9 @@ static int setup_face(const float *verts, const int32_t *face3, int V, int W, in
             const float *a = poly[i], *c = poly[(i + 1) % n];
             float da = plane_dist(p, a, gx, gy), dc = plane_dist(p, c, gx, gy);
             int ina = da >= 0.0f, inc = dc >= 0.0f;
+            /* R5 vertex cap: more than 8 vertices -- only when rounding near w = 0 makes the
+             * polygon non-convex -- culls the face */
+            if (ina + (ina != inc) > 8 - m) return 0;
             if (ina) { memcpy(tmp[m], a, sizeof(tmp[m])); ++m; }
             if (ina != inc) {
                 float t = da / (da - dc);

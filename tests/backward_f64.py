@@ -94,6 +94,9 @@ class Tri:
         return lam, Wm
 
 
+CAP_CULLS = [0]  # faces culled by R5's vertex cap so far (tests)
+
+
 def _plane(p, v, gx, gy):
     x, y, z, w = v[0], v[1], v[2], v[3]
     return (z + w, gx * w + x, gx * w - x, gy * w + y, gy * w - y)[p]
@@ -117,6 +120,9 @@ def setup_face(verts, face, V, W, H):
         for i in range(n):
             a, c = poly[i], poly[(i + 1) % n]
             da, dc = _plane(pl, a, gx, gy), _plane(pl, c, gx, gy)
+            if (da >= 0) + ((da >= 0) != (dc >= 0)) > 8 - len(out):  # R5 vertex cap: more than 8 culls the face
+                CAP_CULLS[0] += 1
+                return [], True
             if da >= 0:
                 out.append(a)
             if (da >= 0) != (dc >= 0):

@@ -230,6 +230,47 @@ def fullscreen_quad():
     return v, f
 
 
+def near_w0_scene(seed, W=64, H=48, C=3, F=160):
+    """Clipping stress around w = 0, where R5's plane intersections lose their guard-band guarantee (fuzz seed
+    167059): faces with one or two vertices at |w| log-uniform in [1e-14, 1e-2] (either sign) and x, y up to
+    1e4 |w| (far outside the guard band) or exactly on a guard plane, near-duplicate copies shifted by a few
+    ulps (the seed's two faces), and ordinary faces for the depth test to compete with."""
+    rng = np.random.default_rng(seed)
+    gx, gy = 32768.0 / W, 32768.0 / H
+    tris = []
+    for _ in range(F):
+        kind = rng.integers(0, 5)
+        if kind == 4 and tris:  # near-duplicate of an earlier face: every coordinate nudged by a few ulps
+            base = np.array(tris[rng.integers(0, len(tris))], np.float32)
+            tris.append((base * (1 + rng.integers(-4, 5, size=base.shape) * np.float32(2 ** -23))).tolist())
+            continue
+        t = []
+        nsmall = rng.integers(1, 3)
+        for k in range(3):
+            if k < nsmall:
+                w = 10.0 ** rng.uniform(-14, -2) * rng.choice([-1.0, 1.0, 1.0])
+                if rng.uniform() < 0.3:  # on a guard plane
+                    x, y = rng.choice([-gx, gx]) * abs(w), rng.uniform(-gy, gy) * abs(w)
+                else:
+                    x, y = rng.uniform(-1e4, 1e4, 2) * abs(w)
+                z = rng.uniform(-1.5, 1.5) * abs(w)
+            else:
+                w = rng.uniform(0.3, 2.0)
+                x, y = rng.uniform(-1.2, 1.2, 2) * w
+                z = rng.uniform(-0.9, 0.9) * w
+            t.append([x, y, z, w])
+        tris.append([t[i] for i in rng.permutation(3)])
+    for _ in range(F // 4):  # ordinary faces
+        p = rng.uniform(-1, 1, size=(3, 2))
+        z = rng.uniform(-0.9, 0.9)
+        tris.append([[p[k, 0], p[k, 1], z, 1.0] for k in range(3)])
+    v = np.array(tris, np.float64).reshape(-1, 4).astype(np.float32)
+    faces = np.arange(len(v), dtype=np.int32).reshape(-1, 3)
+    cols = rng.uniform(0, 1, size=(len(v), C)).astype(np.float32)
+    bg = rng.uniform(0, 1, size=(H, W, C)).astype(np.float32)
+    return bg, v, cols, faces
+
+
 def adversarial_scene(seed, W=64, H=48, C=3, F=300):
     """Fuzz scene for the raster rules' edge cases, mixed at random: vertices snapped to pixel centres and
     pixel edges (top-left rule ties), axis-aligned edges, fans sharing edges, slivers, sub-pixel

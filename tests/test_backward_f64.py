@@ -72,6 +72,17 @@ def test_f64_pin_sub_vertex_beyond_guard_band():
     check_pin(bg, v, c, f, 167059)
 
 
+def test_f64_pin_clip_vertex_cap():
+    """scenes.near_w0_scene seed 41533: a face whose clipped polygon exceeds 8 vertices (rounding near w = 0);
+    R5's vertex cap culls it in the oracle and in the float64 statement alike."""
+    bg, v, c, f = (a[None] for a in scenes.near_w0_scene(41533, W=33, H=17, C=1))
+    before = backward_f64.CAP_CULLS[0]
+    for fi in range(f.shape[1]):
+        backward_f64.setup_face(v[0], f[0][fi], v.shape[1], 33, 17)
+    assert backward_f64.CAP_CULLS[0] > before
+    check_pin(bg, v, c, f, 41533)
+
+
 @pytest.mark.parametrize("block", range(5))
 def test_f64_pin_clipped_slivers(block):
     """50 scenes of guard-band and near-plane clipped slivers (10 per case)."""

@@ -450,6 +450,26 @@ def test_clipped_sub_vertex_beyond_guard_band():
     check_scene(*scenes.fuzz_case(167059), seed=167059)
 
 
+def test_clip_polygon_vertex_cap():
+    """near_w0_scene seed 41533: rounding near w = 0 makes a clipped polygon non-convex, and Sutherland-Hodgman
+    produced more than the 8 vertices a convex one can have (the oracle overran its polygon buffer; the kernel
+    would have written past its private arrays and the face's 6 record slots).  R5's vertex cap culls such a
+    face on every side."""
+    seed = 41533
+    check_scene(*scenes.near_w0_scene(seed, W=33, H=17, C=1), seed=seed)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_W0_FUZZ_FIRST", "0")),
+                                         int(os.environ.get("DIRT_W0_FUZZ_SEEDS", "8"))))
+def test_fuzz_near_w0_clipping(seed):
+    """Clipping stress around w = 0 (scenes.near_w0_scene: tiny |w| of either sign, coordinates far outside the
+    guard band or on a guard plane, near-duplicate faces); three frame shapes, 1..8 channels.
+    DIRT_W0_FUZZ_SEEDS=N widens it to the seeds below N (default 8), from DIRT_W0_FUZZ_FIRST."""
+    W, H = [(64, 48), (33, 17), (130, 70), (1024, 8)][seed % 4]
+    C = (3, 1, 7, 5)[seed % 4]
+    check_scene(*scenes.near_w0_scene(seed, W=W, H=H, C=C), seed=seed)
+
+
 def test_extreme_w_and_constant_depth_faces():
     """Setup's division shortcuts fall back to plain IEEE division outside 2^-60 <= |x| <= 2^60 and for zero
     numerators: faces whose clip coordinates are scaled by 1e-20 / 1e20 (same projection, w outside the
