@@ -463,11 +463,13 @@ def test_clip_polygon_vertex_cap():
                                          int(os.environ.get("DIRT_W0_FUZZ_SEEDS", "8"))))
 def test_fuzz_near_w0_clipping(seed):
     """Clipping stress around w = 0 (scenes.near_w0_scene: tiny |w| of either sign, coordinates far outside the
-    guard band or on a guard plane, near-duplicate faces); three frame shapes, 1..8 channels.
+    guard band or on a guard plane, near-duplicate faces); four frame shapes, 1..8 channels, every fifth seed
+    small enough for the fused forward.
     DIRT_W0_FUZZ_SEEDS=N widens it to the seeds below N (default 8), from DIRT_W0_FUZZ_FIRST."""
     W, H = [(64, 48), (33, 17), (130, 70), (1024, 8)][seed % 4]
     C = (3, 1, 7, 5)[seed % 4]
-    check_scene(*scenes.near_w0_scene(seed, W=W, H=H, C=C), seed=seed)
+    F = 24 if seed % 5 == 4 else 160  # 30 faces in all: the fused small-scene forward (clip_face into LDS)
+    check_scene(*scenes.near_w0_scene(seed, W=W, H=H, C=C, F=F), seed=seed)
 
 
 def test_extreme_w_and_constant_depth_faces():
