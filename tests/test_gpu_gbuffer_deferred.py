@@ -56,6 +56,16 @@ def test_gbuffer_outputs_bit_exact(name):
     assert np.abs(bary[cov].sum(-1) - 1.0).max() < 1e-5
 
 
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_GBUF_W0_FIRST", "0")),
+                                         int(os.environ.get("DIRT_GBUF_W0_SEEDS", "4"))))
+def test_gbuffer_outputs_near_w0_fuzz(seed):
+    """The G-buffer outputs (depth, barycentrics of clipped faces' parents, face ids) on the clipping stress
+    scenes around w = 0 (scenes.near_w0_scene), bit-exact against the oracle.  DIRT_GBUF_W0_SEEDS=N widens it
+    to the seeds below N (default 4), from DIRT_GBUF_W0_FIRST."""
+    W, H = [(64, 48), (33, 17), (130, 70), (1024, 8)][seed % 4]
+    _gbuffer_scene(*scenes.near_w0_scene(500000 + seed, W=W, H=H, C=(3, 1, 7, 5)[seed % 4]))
+
+
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_GBUF_FUZZ_FIRST", "0")),
                                          int(os.environ.get("DIRT_GBUF_FUZZ_SEEDS", "12"))))
 def test_gbuffer_outputs_adversarial_fuzz(seed):
