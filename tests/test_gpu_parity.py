@@ -473,12 +473,11 @@ def test_fuzz_near_w0_clipping(seed):
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_W0X_FUZZ_FIRST", "0")),
-                                         int(os.environ.get("DIRT_W0X_FUZZ_SEEDS", "0"))))
+                                         int(os.environ.get("DIRT_W0X_FUZZ_SEEDS", "4"))))
 def test_fuzz_near_w0_clipping_extreme_frames(seed):
     """The near-w0 clipping stress on frames at the size limit in one dimension (8192 x 4, 4 x 8192 and odd
     sizes): the narrowest guard bands (gx = 32768 / W = 4) and the largest snapped coordinates.
-    DIRT_W0X_FUZZ_SEEDS=N runs the seeds below N (default none: a campaign, not a suite case), from
-    DIRT_W0X_FUZZ_FIRST."""
+    DIRT_W0X_FUZZ_SEEDS=N widens it to the seeds below N (default 4), from DIRT_W0X_FUZZ_FIRST."""
     W, H = [(8192, 4), (4, 8192), (8191, 3), (5, 8191)][seed % 4]
     check_scene(*scenes.near_w0_scene(700000 + seed, W=W, H=H, C=(3, 1, 7, 5)[seed % 4], F=80), seed=seed)
 
