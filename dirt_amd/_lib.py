@@ -27,7 +27,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes
@@ -54,6 +54,7 @@ SIGNATURES = {
                                           _P]),
     "dirt_scratch_clear": (_I, [_I, _I, _I, _I, _I64, _P, _SZ, _P]),
     "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
+    "dirt_stream_capture_id": (_I, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
     "dirt_profile_enable": (_I, [_I]),
     "dirt_profile_read": (_I, [_I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double)]),
     "dirt_vertex_normals_fwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _P]),
@@ -120,6 +121,27 @@ def recompute_workspace_size(B, H, W, C, V, F):
     n = ctypes.c_size_t(0)
     check(load().dirt_bwd_recompute_workspace_size(B, H, W, C, V, F, ctypes.byref(n)))
     return n.value
+
+
+def capture_id(stream):
+    """Id of the HIP graph capture `stream` (a hipStream_t handle) is recording, 0 when none."""
+    cid = ctypes.c_ulonglong(0)
+    check(load().dirt_stream_capture_id(stream, ctypes.byref(cid)))
+    return cid.value
+
+
+def clip_stats(B, H, W, F, bin_capacity, scratch, scratch_bytes, stream, reset=True):
+    """Debug (synchronises `stream`): the R5 deviation counters a forward scratch holds, summed since it was last
+    cleared -- {"cap_culled": faces culled by the R5 vertex cap, "clamped": clipped faces whose sub-vertices the
+    R5 clamp moved}.  `scratch` is a device pointer; reset zeroes the counters afterwards."""
+    lib = load()
+    fn = lib.dirt_debug_clip_stats
+    fn.restype = ctypes.c_int
+    fn.argtypes = [_I, _I, _I, _I, _I64, _P, _SZ, _P, _I, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    cap, clamped = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    check(fn(B, H, W, F, bin_capacity, scratch, scratch_bytes, stream, 1 if reset else 0, ctypes.byref(cap),
+             ctypes.byref(clamped)))
+    return {"cap_culled": cap.value, "clamped": clamped.value}
 
 
 NUM_KERNELS = 3

@@ -245,7 +245,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 9; }
+int dirt_abi_version(void) { return 10; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -597,6 +597,32 @@ int dirt_debug_bin_occupancy(int B, int H, int W, int F, int64_t bin_capacity, c
     return DIRT_OK;
 }
 
+// Debug (synchronises `stream`): the R5 deviation counters of `scratch` (setup_kernel.h kStatCapCulled /
+// kStatClamped), summed over every forward since the scratch was last cleared: faces culled by the R5 vertex cap
+// and clipped faces whose sub-vertices the R5 clamp moved.  reset != 0 zeroes them afterwards.  Not part of
+// include/dirt_mi355x.h.
+int dirt_debug_clip_stats(int B, int H, int W, int F, int64_t bin_capacity, void *scratch, size_t scratch_bytes,
+                          void *stream_, int reset, uint32_t *cap_culled, uint32_t *clamped)
+{
+    Layout L;
+    int rc = make_layout(B, H, W, F, bin_capacity, L);
+    if (rc) return rc;
+    if (!scratch || scratch_bytes < L.scratch_total) return fail(DIRT_EINVAL, "dirt_debug_clip_stats: scratch too small");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(static_cast<char *>(scratch) + L.off_flag);
+    uint32_t h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&h[0], flag + kStatCapCulled, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&h[1], flag + kStatClamped, 4, hipMemcpyDeviceToHost, stream));
+    if (reset) {
+        HIP_TRY(hipMemsetAsync(flag + kStatCapCulled, 0, 4, stream));
+        HIP_TRY(hipMemsetAsync(flag + kStatClamped, 0, 4, stream));
+    }
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (cap_culled) *cap_culled = h[0];
+    if (clamped) *clamped = h[1];
+    return DIRT_OK;
+}
+
 // Ablation entry point (tools/ablate.py): re-runs raster_kernel (C == 3) on the bins a preceding
 // dirt_rasterise_fwd left in `scratch`, with parts switched off; returns the kernel time in ms.
 int dirt_debug_raster_variant(int variant, const float *background, const float *vertices, const float *vertex_colors,
@@ -801,6 +827,16 @@ int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *s
         return fail(DIRT_EINVAL, "dirt_scratch_clear: scratch smaller than dirt_workspace_sizes()");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     HIP_TRY(hipMemsetAsync(static_cast<char *>(scratch) + L.off_count, 0, L.off_bins - L.off_count, stream));
+    return DIRT_OK;
+}
+
+int dirt_stream_capture_id(void *stream_, unsigned long long *capture_id)
+{
+    if (!capture_id) return fail(DIRT_EINVAL, "dirt_stream_capture_id: null pointer");
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    HIP_TRY(hipStreamGetCaptureInfo(reinterpret_cast<hipStream_t>(stream_), &st, &id));
+    *capture_id = st == hipStreamCaptureStatusActive ? id : 0ull;
     return DIRT_OK;
 }
 

@@ -293,6 +293,9 @@ __device__ __forceinline__ uint32_t entry_occluder_qmax(const StripEntry *ent, u
         const int4v q0 = ve[0], q1 = ve[1];
         const int e[3] = {q0.x, q0.y, q0.z};
         const uint32_t ab[3] = {(uint32_t)q0.w, (uint32_t)q1.x, (uint32_t)q1.y};
+        // a large entry keeps its record index in e[0] and the kLargeAB sentinel in ab[0]; its other fields are
+        // not edge values of this tile, so it is never taken as an occluder
+        cover = ab[0] != kLargeAB;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int A = (int)(short)(ab[k] & 0xffffu), B = (int)(short)(ab[k] >> 16);
@@ -568,22 +571,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
 #ifndef DIRT_RASTER_REMAT_IJ
 #define DIRT_RASTER_REMAT_IJ 1
 #endif
-#if DIRT_RASTER_REMAT_IJ
-    const int i0_ = tx * kTile + lx, j0_ = ty * kTile + ly;  // (the resolve recomputes them)
-#define i i0_
-#define j j0_
-#else
-    const int i = tx * kTile + lx, j = ty * kTile + ly;
-#endif
+    const int pi = tx * kTile + lx, pj = ty * kTile + ly;  // this lane's pixel (the resolve recomputes it: i, j)
     const int dx = lx * 256, dy = ly * 256;  // offset from the tile origin (sub-pixels)
-    const float fxl = (float)i + 0.5f, fyl = (float)j + 0.5f;
+    const float fxl = (float)pi + 0.5f, fyl = (float)pj + 0.5f;
     const Rec *frame_recs = FUSED ? s_recs : recs + (int64_t)b * nrec;
     const FaceData *fdata_frame = FUSED ? s_fd : fdata + (int64_t)b * F;
     if constexpr (FUSED) {
         if (t < F) {
             bool oob;
+            // (only the workgroup of tile 0 counts the R5 deviations: every workgroup repeats the frame's setup)
             s_fd[t] = setup_face_into(verts + (int64_t)b * V * 4, faces + ((int64_t)b * F + t) * 3, V, F, W, H, t,
-                                      s_recs, oob);
+                                      s_recs, oob, blockIdx.x == 0 ? flag : nullptr);
             if (oob) atomicOr(flag, 1u);
         }
         __syncthreads();
@@ -787,8 +785,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                         for (int k = base; k < base + seg; k += 2) {
                             const EntryRegs qa = load_entry_at(t_ent, oo.x), qb = load_entry_at(t_ent, oo.y);
                             oo = *(lds_u32x2 *)&t_wl[wave][k + 2];
-                            raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, i, j, best);
-                            raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, i, j, best);
+                            raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, pi, pj, best);
+                            raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, pi, pj, best);
                         }
                         if (kNoDepth || !DIRT_RASTER_HZ || rp >= ns) break;
 #if DIRT_RASTER_HZ
@@ -807,7 +805,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     }
                     for (int k = 0; k < nl; ++k)
                         raster_entry<kNoDepth, true>(load_entry(t_ent, (int)t_wl[wave][kWaveList - 1 - k]), frame_recs, pix,
-                                                     pxy, i, j, best);
+                                                     pxy, pi, pj, best);
                 } else if (nst > 0) {
                     best += t_ent[lane % nst].key;
                 }
@@ -826,10 +824,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                     const int e1 = c0 + (int)__builtin_ctzll(mine);
                                     mine &= mine - 1;
                                     const EntryRegs qa = load_entry(t_ent, e0), qb = load_entry(t_ent, e1);
-                                    raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, i, j, best);
-                                    raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, i, j, best);
+                                    raster_entry<kNoDepth, false>(qa, frame_recs, pix, pxy, pi, pj, best);
+                                    raster_entry<kNoDepth, false>(qb, frame_recs, pix, pxy, pi, pj, best);
                                 } else {
-                                    raster_entry<kNoDepth, false>(load_entry(t_ent, e0), frame_recs, pix, pxy, i, j, best);
+                                    raster_entry<kNoDepth, false>(load_entry(t_ent, e0), frame_recs, pix, pxy, pi, pj, best);
                                 }
                             }
                         } else {
@@ -838,9 +836,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                 mine &= mine - 1;
                                 const EntryRegs q = load_entry(t_ent, c0 + bit);
                                 if ((big >> bit) & 1)
-                                    raster_entry<kNoDepth, true>(q, frame_recs, pix, pxy, i, j, best);
+                                    raster_entry<kNoDepth, true>(q, frame_recs, pix, pxy, pi, pj, best);
                                 else
-                                    raster_entry<kNoDepth, false>(q, frame_recs, pix, pxy, i, j, best);
+                                    raster_entry<kNoDepth, false>(q, frame_recs, pix, pxy, pi, pj, best);
                             }
                         }
                     }
@@ -866,8 +864,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     }
     PHASE_TS(3);
 #if DIRT_RASTER_REMAT_IJ
-#undef i
-#undef j
     // the lane's pixel again, from an opaque copy of threadIdx.x: the compiler cannot reuse the values computed
     // before the chunk loop, so they need not stay live (in VGPRs) across it
     int i, j;
@@ -878,6 +874,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         i = tx * kTile + wave_ox(wave2) + lane2 % kWaveW;
         j = ty * kTile + wave_oy(wave2) + lane2 / kWaveW;
     }
+#else
+    const int i = pi, j = pj;
 #endif
     // (the pixel's offset is computed here, after the chunk loop: live across it, it cost a VGPR spill)
     if (!(i < W && j < H)) return;

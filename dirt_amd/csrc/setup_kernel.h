@@ -24,9 +24,17 @@ __device__ inline float plane_dist(int p, const float *v, float gx, float gy)
 constexpr int kMaxClipVerts = 8;
 static_assert(kMaxClipVerts - 2 == kExtraPerFace + 1, "sub-triangle slots");
 
+// R5 deviation counters, words of the scratch's flag area (cleared with the bin counters,
+// cumulative until then; dirt_debug_clip_stats reads them): faces culled by the R5 vertex cap, and clipped faces
+// with at least one sub-vertex moved by the R5 sub-vertex clamp.  A GL driver keeps both kinds of face (it has no
+// fixed polygon buffer and clips in higher precision), so these count where this rasteriser's output may differ
+// from the reference's for reasons other than driver arithmetic.  Only the clipping slow path touches them.
+constexpr int kStatCapCulled = 48, kStatClamped = 52;
+
 // R5 slow path: clip against z>=-w and the guard planes, fan-triangulate, write the sub-records.
-// Not inlined so that its stack arrays do not inflate the fast path.  Returns nsub.
-__device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *frame_recs)
+// Not inlined so that its stack arrays do not inflate the fast path.  Returns nsub.  `flag`: the scratch's
+// flag area (the R5 deviation counters above), may be null.
+__device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *frame_recs, uint32_t *flag)
 {
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
     float poly[kMaxClipVerts][7], tmp[kMaxClipVerts][7];
@@ -44,7 +52,10 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
             const bool ina = da >= 0.0f, inc = dc >= 0.0f;
             // R5 vertex cap: more than 8 vertices (possible only when rounding near w = 0 makes the polygon
             // non-convex) culls the face -- it would need more than the 6 sub-triangle slots
-            if ((ina ? 1 : 0) + (ina != inc ? 1 : 0) > kMaxClipVerts - m) return 0;
+            if ((ina ? 1 : 0) + (ina != inc ? 1 : 0) > kMaxClipVerts - m) {
+                if (flag) atomicAdd(&flag[kStatCapCulled], 1u);
+                return 0;
+            }
             if (ina) {
                 for (int q = 0; q < 7; ++q) tmp[m][q] = a[q];
                 ++m;
@@ -63,6 +74,15 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
     for (int i = 0; i < n; ++i)
         if (!(poly[i][3] > 0.0f)) return 0;
     const int nsub = n - 2;
+    if (flag) {
+        // the sub-vertex clamp of make_record<true> (the same quotients): does it move any sub-vertex?
+        bool moved = false;
+        for (int i = 0; i < n; ++i) {
+            const float iw = 1.0f / poly[i][3], xn = poly[i][0] * iw, yn = poly[i][1] * iw;
+            moved = moved || guard_clamp(xn, 2.0f * gx) != xn || guard_clamp(yn, 2.0f * gy) != yn;
+        }
+        if (moved) atomicAdd(&flag[kStatClamped], 1u);
+    }
     for (int s = 0; s < nsub; ++s) {
         float sv[3][4], sb[3][3];
         const int idx[3] = {0, s + 1, s + 2};
@@ -81,7 +101,7 @@ __device__ __noinline__ int clip_face(Tri tri, int W, int H, int F, int f, Rec *
 // fused small-scene raster passes LDS): the fast-path record at slot f, or the clipped sub-records.
 // Returns the face's FaceData; `oob` = a vertex index outside [0, V) (the face is culled).
 __device__ __forceinline__ FaceData setup_face_into(const float *vb, const int32_t *face3, int V, int F, int W, int H,
-                                                    int f, Rec *frame_recs, bool &oob)
+                                                    int f, Rec *frame_recs, bool &oob, uint32_t *flag)
 {
     const float gx = 32768.0f / (float)W, gy = 32768.0f / (float)H;
     const int32_t vidx[3] = {face3[0], face3[1], face3[2]};
@@ -119,7 +139,7 @@ __device__ __forceinline__ FaceData setup_face_into(const float *vb, const int32
     } else {
         frame_recs[f] = r;  // empty unless clip_face overwrites it
         if (ok) {
-            nsub = clip_face(tri, W, H, F, f, frame_recs);
+            nsub = clip_face(tri, W, H, F, f, frame_recs, flag);
             fd.clipped = 1;
         }
     }
@@ -370,7 +390,7 @@ __global__ __launch_bounds__(NT) void setup_kernel(const float *__restrict__ ver
             frame_recs[f] = r;  // empty unless clip_face overwrites it
 #ifndef DIRT_SETUP_NO_CLIP
             if (ok) {
-                nsub = clip_face(tri, W, H, F, f, frame_recs);
+                nsub = clip_face(tri, W, H, F, f, frame_recs, flag);
                 fd.clipped = 1;
             }
 #endif

@@ -33,6 +33,7 @@ struct Api {
     decltype(&dirt_rasterise_bwd) bwd = nullptr;
     decltype(&dirt_scratch_clear) scratch_clear = nullptr;
     decltype(&dirt_check_faces) check_faces = nullptr;
+    decltype(&dirt_stream_capture_id) capture_id = nullptr;
     decltype(&dirt_last_error) last_error = nullptr;
     decltype(&dirt_vertex_normals_fwd) vn_fwd = nullptr;
     decltype(&dirt_vertex_normals_bwd) vn_bwd = nullptr;
@@ -68,6 +69,7 @@ void init(const std::string &path)
     g_api.bwd = reinterpret_cast<decltype(g_api.bwd)>(sym("dirt_rasterise_bwd"));
     g_api.scratch_clear = reinterpret_cast<decltype(g_api.scratch_clear)>(sym("dirt_scratch_clear"));
     g_api.check_faces = reinterpret_cast<decltype(g_api.check_faces)>(sym("dirt_check_faces"));
+    g_api.capture_id = reinterpret_cast<decltype(g_api.capture_id)>(sym("dirt_stream_capture_id"));
     g_api.last_error = reinterpret_cast<decltype(g_api.last_error)>(sym("dirt_last_error"));
     g_api.vn_fwd = reinterpret_cast<decltype(g_api.vn_fwd)>(sym("dirt_vertex_normals_fwd"));
     g_api.vn_bwd = reinterpret_cast<decltype(g_api.vn_bwd)>(sym("dirt_vertex_normals_bwd"));
@@ -81,65 +83,78 @@ void init(const std::string &path)
 
 // Forward-only scratch (bins, bin counters) per (device, stream, layout), cleared once: every forward
 // leaves it clean for the next one of the same layout (DIRT_FWD_SCRATCH_CLEAN).  LRU of a few layouts.
-// An entry used while its stream is capturing a HIP graph is pinned (the graph's replays write it and nothing
-// else holds a reference): eviction and clear() skip it, clear(force) drops it.  An entry whose forward failed
-// is discarded (its alternating count sets may be dirty).
+// Graph capture: a scratch created while the stream captures a HIP graph comes from that graph's
+// private memory pool and is cleared by a memset captured into the graph, i.e. it is clean only for that graph's
+// replays.  Those entries are keyed by the capture id too (dirt_stream_capture_id) and kept apart: forwards of
+// one capture share one, no other capture or eager call sees it, and dropping the cache's reference is safe at
+// any time (the block stays in the graph's pool).  An entry whose forward failed is discarded (its alternating
+// count sets may be dirty).  The Python twin is dirt_amd.rasterise_ops._Workspace.
 struct ScratchCache {
     typedef std::tuple<int, uintptr_t, int64_t, int64_t, int64_t, int64_t, int64_t> Key;
     struct Entry {
         Key key;
         at::Tensor t;
-        bool pinned;
     };
     std::mutex mu;
-    std::list<Entry> lru;
-    static bool capturing(hipStream_t stream)
+    std::list<Entry> lru;             // eager entries
+    unsigned long long cap_id = 0;    // the capture the entries below belong to
+    std::list<Entry> cap;
+    static unsigned long long capture_id(hipStream_t stream)
     {
         hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-        return hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+        if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusActive) return 0;
+        unsigned long long id = 0;
+        check(g_api.capture_id(stream, &id));
+        return id;
     }
-    void evict()
+    static at::Tensor *find(std::list<Entry> &l, const Key &k, bool to_front)
     {
-        size_t n = lru.size();
-        for (auto it = lru.end(); n > 4 && it != lru.begin();) {
-            --it;
-            if (!it->pinned) {
-                it = lru.erase(it);
-                --n;
+        for (auto it = l.begin(); it != l.end(); ++it)
+            if (it->key == k) {
+                if (to_front) l.splice(l.begin(), l, it);
+                return to_front ? &l.front().t : &it->t;
             }
-        }
+        return nullptr;
     }
     at::Tensor get(const Key &k, size_t bytes, const at::Device &dev, hipStream_t stream)
     {
-        const bool cap = capturing(stream);
-        std::lock_guard<std::mutex> g(mu);
-        for (auto it = lru.begin(); it != lru.end(); ++it)
-            if (it->key == k) {
-                it->pinned = it->pinned || cap;
-                lru.splice(lru.begin(), lru, it);
-                return lru.front().t;
+        const unsigned long long cid = capture_id(stream);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (cid && cid != cap_id) {  // a new capture: the previous one's entries belong to its graph now
+                cap_id = cid;
+                cap.clear();
             }
+            if (at::Tensor *t = find(cid ? cap : lru, k, !cid)) return *t;
+        }
         at::Tensor t = at::empty({(int64_t)std::max<size_t>(bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
         check(g_api.scratch_clear((int)std::get<2>(k), (int)std::get<3>(k), (int)std::get<4>(k), (int)std::get<5>(k),
                                   std::get<6>(k), t.data_ptr(), bytes, stream));
-        lru.push_front(Entry{k, t, cap});
-        evict();
+        std::lock_guard<std::mutex> g(mu);
+        if (cid) {
+            if (cid == cap_id) cap.push_front(Entry{k, t});
+        } else {
+            lru.push_front(Entry{k, t});
+            while (lru.size() > 4) lru.pop_back();
+        }
         return t;
     }
     void discard(const Key &k)
     {
         std::lock_guard<std::mutex> g(mu);
         lru.remove_if([&](const Entry &e) { return e.key == k; });
+        cap.remove_if([&](const Entry &e) { return e.key == k; });
     }
-    void clear(bool force)
+    void clear(bool)
     {
         std::lock_guard<std::mutex> g(mu);
-        lru.remove_if([&](const Entry &e) { return force || !e.pinned; });
+        lru.clear();
+        cap.clear();
     }
     size_t size()
     {
         std::lock_guard<std::mutex> g(mu);
-        return lru.size();
+        return lru.size() + cap.size();
     }
 } g_scratch;
 
@@ -348,6 +363,17 @@ at::Tensor grad_or_zeros(const at::Tensor &g, const at::Tensor &like)
     return g.defined() ? g.to(at::kFloat).contiguous() : at::zeros_like(like);
 }
 
+// The fused helpers' backwards are raw kernels: their results carry no graph, so a second-order gradient
+// (create_graph=True, e.g. a gradient penalty) through them would be silently missing.  Refuse it instead
+// (ADVICE r4); DIRT_FUSED_LIGHTING=0 routes dirt_amd.lighting to its framework-op statement, which supports it.
+void no_double_backward(const char *fn)
+{
+    if (at::GradMode::is_enabled())
+        throw std::runtime_error(std::string(fn) +
+                                 ": the fused HIP backward does not support create_graph=True (double backward); "
+                                 "set DIRT_FUSED_LIGHTING=0 to use the framework-op statement");
+}
+
 struct VertexNormalsFn : public torch::autograd::Function<VertexNormalsFn> {
     // vertices [*, V, D >= 3] contiguous (only x, y, z read), faces [F, 3] int32 / int64
     static at::Tensor forward(AutogradContext *ctx, at::Tensor vertices, at::Tensor faces)
@@ -365,6 +391,7 @@ struct VertexNormalsFn : public torch::autograd::Function<VertexNormalsFn> {
     }
     static variable_list backward(AutogradContext *ctx, variable_list grads)
     {
+        no_double_backward("vertex_normals");
         auto sv = ctx->get_saved_variables();
         const at::Tensor &vertices = sv[0], &faces = sv[1], &summed = sv[2];
         c10::hip::HIPGuard guard(vertices.device().index());
@@ -394,6 +421,7 @@ struct DiffuseFn : public torch::autograd::Function<DiffuseFn> {
     }
     static variable_list backward(AutogradContext *ctx, variable_list grads)
     {
+        no_double_backward("diffuse_directional");
         auto sv = ctx->get_saved_variables();
         const at::Tensor &normals = sv[0], &colors = sv[1];
         c10::hip::HIPGuard guard(normals.device().index());
@@ -423,6 +451,7 @@ struct DiffusePointFn : public torch::autograd::Function<DiffusePointFn> {
     }
     static variable_list backward(AutogradContext *ctx, variable_list grads)
     {
+        no_double_backward("diffuse_point");
         auto sv = ctx->get_saved_variables();
         const at::Tensor &positions = sv[0], &normals = sv[1], &colors = sv[2];
         c10::hip::HIPGuard guard(positions.device().index());
@@ -457,6 +486,7 @@ struct SpecularFn : public torch::autograd::Function<SpecularFn> {
     }
     static variable_list backward(AutogradContext *ctx, variable_list grads)
     {
+        no_double_backward("specular_directional");
         auto sv = ctx->get_saved_variables();
         const at::Tensor &positions = sv[0], &normals = sv[1], &refl = sv[2];
         c10::hip::HIPGuard guard(positions.device().index());

@@ -11,7 +11,14 @@ dirt_vertex_normals_* / dirt_diffuse_directional_* / dirt_specular_directional_*
 their operands are float32 tensors on one GPU, of one [..., 3] shape, with light parameters of shape [3] that need no gradient and a Python-number
 shininess; anything else -- CPU tensors, broadcasting, gradients with respect to the light -- runs the
 framework-op statement below (`_*_ops`), which is also the fused kernels' fp32 test reference.
+
+The fused backwards are kernels, not differentiable graphs: a second-order gradient through them
+(`create_graph=True`) raises RuntimeError rather than silently dropping terms.  DIRT_FUSED_LIGHTING=0 routes every
+call to the framework ops (double backward supported).  Out-of-range face indices: the fused vertex_normals skips
+such faces; the framework statement's index_select rejects them (on a GPU as a device-side assert).
 """
+import os
+
 import torch
 
 __all__ = ["vertex_normals", "vertex_normals_pre_split", "split_vertices_by_face", "diffuse_directional",
@@ -34,8 +41,14 @@ def _get_face_normals(vertices, faces):
     return normals / (torch.linalg.norm(normals, dim=-1, keepdim=True) + 1.e-12)
 
 
+_FUSED_ENABLED = os.environ.get("DIRT_FUSED_LIGHTING", "1") != "0"
+
+
 def _fused():
-    """The C++ extension bound to the HIP library (None if not built: the framework ops run)."""
+    """The C++ extension bound to the HIP library (None if not built or DIRT_FUSED_LIGHTING=0: the framework ops
+    run)."""
+    if not _FUSED_ENABLED:
+        return None
     from .rasterise_ops import _torch_ext
     return _torch_ext()
 

@@ -70,68 +70,68 @@ class _Workspace:
     counter memset (128 MiB for B = 64 at 8192^2 with one 256-B line per counter) and the allocation.
     Keyed by the stream too: two streams never share a scratch.  A few layouts are kept (LRU).
 
-    Graph capture: a HIP graph captured through the op replays writes into this scratch, and neither the
-    autograd context nor the graph holds a reference to it, so an entry used while its stream was capturing is
-    pinned: LRU eviction and clear() skip it (clear(force=True) drops it too, for callers that have destroyed
-    their graphs).  An entry whose forward failed after its first launch is dropped (`discard`): its
-    alternating bin-count sets may no longer be clean."""
+    Graph capture: a scratch created while a stream captures a HIP graph is allocated from that
+    graph's private memory pool and cleared by a memset captured into that graph, so it is clean only for that
+    graph's replays.  Such entries are keyed by the capture id as well (`dirt_stream_capture_id`): forwards of
+    one capture share one scratch, and no other capture or eager call ever sees it (a second graph of the same
+    layout gets its own, cleared by its own replays -- whichever graph replays first).  Eager entries are never
+    handed to a capture either.  Dropping the cache's reference to a capture's scratch is safe at any time: the
+    block stays in the graph's private pool, which only that graph's replays use.  An entry whose forward
+    failed after its first launch is dropped (`discard`): its alternating bin-count sets may no longer be
+    clean."""
 
     def __init__(self, keep=4):
         self.keep = keep
         self._lock = threading.Lock()
         self._d = collections.OrderedDict()
-        self._pinned = set()
+        self._cap_id = 0
+        self._cap = {}
 
     def scratch(self, dev, stream, layout, nbytes):
+        cid = _lib.capture_id(stream) if torch.cuda.is_current_stream_capturing() else 0
         key = (dev, stream, layout)
-        capturing = torch.cuda.is_current_stream_capturing()
         with self._lock:
-            t = self._d.get(key)
+            if cid:
+                if cid != self._cap_id:  # a new capture: the previous one's entries are its graph's now
+                    self._cap_id, self._cap = cid, {}
+                t = self._cap.get(key)
+            else:
+                t = self._d.get(key)
+                if t is not None:
+                    self._d.move_to_end(key)
             if t is not None:
-                self._d.move_to_end(key)
-                if capturing:
-                    self._pinned.add(key)
                 return t
-        # (a buffer created during capture comes from the graph's private pool and is cleared once, inside the
-        # graph; each replay's forward leaves it clean for the next, as any forward does)
         # only the bin counters need zeroing (dirt_scratch_clear: a memset of the counter lines); the slabs
-        # are written before they are read
+        # are written before they are read.  Under capture the memset is part of the graph.
         t = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
         B, H, W, F, cap = layout
         _lib.check(_lib.load().dirt_scratch_clear(B, H, W, F, cap, t.data_ptr(), nbytes, stream))
         with self._lock:
-            self._d[key] = t
-            if capturing:
-                self._pinned.add(key)
-            self._evict()
+            if cid:
+                if cid == self._cap_id:
+                    self._cap[key] = t
+            else:
+                self._d[key] = t
+                while len(self._d) > self.keep:
+                    self._d.popitem(last=False)
         return t
-
-    def _evict(self):
-        for k in list(self._d):
-            if len(self._d) <= self.keep:
-                break
-            if k not in self._pinned:
-                del self._d[k]
 
     def discard(self, dev, stream, layout):
         with self._lock:
             key = (dev, stream, layout)
             self._d.pop(key, None)
-            self._pinned.discard(key)
+            self._cap.pop(key, None)
 
     def clear(self, force=False):
+        """Drop every cached scratch (`force` is accepted for compatibility: graph-owned scratch lives in its
+        graph's memory pool, so nothing needs pinning)."""
         with self._lock:
-            if force:
-                self._d.clear()
-                self._pinned.clear()
-            else:
-                for k in list(self._d):
-                    if k not in self._pinned:
-                        del self._d[k]
+            self._d.clear()
+            self._cap = {}
 
     def __len__(self):
         with self._lock:
-            return len(self._d)
+            return len(self._d) + len(self._cap)
 
 
 _workspace = _Workspace()
@@ -335,8 +335,8 @@ def _torch_ext():
 
 
 def workspace_cache_clear(force=False):
-    """Drop the cached per-layout scratch buffers (both implementations).  Buffers a captured HIP graph
-    writes are kept unless `force` (then no graph captured through the op may be replayed again)."""
+    """Drop the cached per-layout scratch buffers (both implementations).  Graphs captured through the op keep
+    working: their scratch lives in the graph's own memory pool (`force` is accepted for compatibility)."""
     _workspace.clear(force)
     ext = _torch_ext()
     if ext is not None:

@@ -53,6 +53,13 @@ class RasteriseSession:
                                                 self.scratch_bytes, torch.cuda.current_stream(dev).cuda_stream))
         self._last_stream = torch.cuda.current_stream(dev)
 
+    def clip_stats(self, reset=True):
+        """R5 deviation counters of this session's forwards since the last reset (synchronises): faces culled by
+        the R5 vertex cap and clipped faces moved by the R5 sub-vertex clamp (0 on ordinary scenes)."""
+        B, H, W, C, V, F = self.dims
+        return _lib.clip_stats(B, H, W, F, self.bin_capacity, self.scratch.data_ptr(), self.scratch_bytes,
+                               self._stream(), reset)
+
     def _stream(self):
         """The current stream's handle, ordered after the stream of the session's previous call."""
         cur = torch.cuda.current_stream(self.device)

@@ -73,7 +73,7 @@ extern "C" {
  * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
  * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer; 8: + dirt_rasterise_bwd_recompute,
  * dirt_bwd_recompute_workspace_size; 9: + the fused lighting helpers dirt_vertex_normals_*,
- * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*) */
+ * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*; 10: + dirt_stream_capture_id) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -180,6 +180,11 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
  * (an async memset of a few KB; lets a caller clear them on another stream, see DIRT_FWD_SCRATCH_CLEAN). */
 int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *scratch, size_t scratch_bytes,
                        void *stream);
+
+/* The id of the HIP graph capture `stream` is recording (hipStreamGetCaptureInfo), 0 when it records none.
+ * A scratch created and cleared inside one capture is clean only for that graph's own replays (its clearing
+ * memset runs when the graph replays), so callers that cache scratch per stream key it by this id too. */
+int dirt_stream_capture_id(void *stream, unsigned long long *capture_id);
 
 /* Debug check (synchronises `stream`): returns DIRT_EFACE if any face index is outside [0,V).  Uses the
  * first 4 bytes of `scratch` as its flag: pass a scratch that no forward is using, or clear it after. */

@@ -224,10 +224,10 @@ def test_hip_graph_capture_of_autograd_path():
 
 @pytest.mark.parametrize("impl", ["ext", "py"])
 def test_captured_graph_survives_cache_eviction_and_clear(impl):
-    """a HIP graph captured through the public op replays writes into the op's cached scratch.
-    After capture, clearing the cache and churning it with other layouts must not free that scratch: the
-    entry is pinned while its stream captured.  Capture, clear + evict + allocate over the freed pool,
-    replay, compare with the eager result."""
+    """a HIP graph captured through the public op replays writes into the op's scratch.  After
+    capture, clearing the cache and churning it with other layouts must not free that scratch (since round 5
+    it lives in the graph's own memory pool).  Capture, clear + evict + allocate over the freed pool, replay,
+    compare with the eager result."""
     from dirt_amd import rasterise_ops
     ext = rasterise_ops._torch_ext()
     if impl == "ext":
@@ -279,6 +279,59 @@ def test_captured_graph_survives_cache_eviction_and_clear(impl):
     del junk, graph
     rasterise_ops.workspace_cache_clear(force=True)
     assert rasterise_ops.workspace_cache_size() == 0
+
+
+@pytest.mark.parametrize("impl", ["ext", "py"])
+def test_two_graphs_same_layout_second_replayed_first(impl):
+    """two graphs captured through the public op with the same layout (torch.cuda.graph's default
+    capture stream, so the same (device, stream, layout) key) must not share a scratch created inside the
+    first capture: that scratch is cleared only by the first graph's replays.  Replay the second graph before
+    the first has ever run, on a dirtied allocator, and compare both with the eager results."""
+    from dirt_amd import rasterise_ops
+    ext = rasterise_ops._torch_ext()
+    if impl == "ext":
+        assert ext is not None
+
+    def op(t0, t1, t2, ft, H, W, C):
+        args = (t0, t1, t2, ft, None, H, W, C, 0, 0, False, False)
+        return ext.rasterise(*args) if impl == "ext" else rasterise_ops._RasteriseFunction.apply(*args)
+
+    rasterise_ops.workspace_cache_clear(force=True)
+    # fill the allocator's free blocks with garbage first, so that an uncleared scratch is not accidentally 0
+    junk = [torch.full((1 << 22,), 0x01010101, dtype=torch.int32, device="cuda") for _ in range(16)]
+    del junk
+    scenes_ = [tuple(a[None] for a in scenes.random_triangles(F=2500, W=160, H=128, radius_px=10.0, seed=s))
+               for s in (90, 91)]
+    B, H, W, C = scenes_[0][0].shape
+    graphs, outs, refs = [], [], []
+    for bg, v, c, f in scenes_:
+        t = [_gpu(a).requires_grad_(True) for a in (bg, v, c)]
+        ft = _gpu(f)
+        g = torch.randn(bg.shape, device="cuda")
+        px, _ = op(t[0], t[1], t[2], ft, H, W, C)
+        refs.append((px.detach().clone(), [x.clone() for x in torch.autograd.grad(px, t, g)]))
+        out = {}
+
+        def step(t=t, ft=ft, g=g, out=out):
+            px, _ = op(t[0], t[1], t[2], ft, H, W, C)
+            out["px"] = px
+            out["grads"] = torch.autograd.grad(px, t, g)
+
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        graphs.append(graph)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for k in (1, 0, 1, 0):
+        graphs[k].replay()
+        torch.cuda.synchronize()
+        assert torch.equal(outs[k]["px"], refs[k][0]), "graph %d: pixels differ from the eager call" % k
+        assert torch.equal(outs[k]["grads"][0], refs[k][1][0])
+        for a, b in zip(outs[k]["grads"][1:], refs[k][1][1:]):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
+    del graphs
+    rasterise_ops.workspace_cache_clear(force=True)
 
 
 def test_session_moves_between_streams():

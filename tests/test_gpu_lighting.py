@@ -136,6 +136,34 @@ def test_light_gradient_falls_back_to_framework_ops():
     assert torch.isfinite(g).all() and float(g.abs().sum()) > 0
 
 
+def test_fused_backward_refuses_double_backward(monkeypatch):
+    """the fused backwards carry no graph, so create_graph=True through them raises instead of
+    silently dropping the second-order terms; with DIRT_FUSED_LIGHTING=0 the framework ops run and support it."""
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    n = torch.nn.functional.normalize(torch.randn((256, 3), device=DEV, generator=gen), dim=-1).requires_grad_(True)
+    c = torch.rand((256, 3), device=DEV, generator=gen).requires_grad_(True)
+    ld = torch.nn.functional.normalize(torch.tensor([1.0, -0.3, -0.5], device=DEV), dim=0)
+    lc = torch.ones(3, device=DEV)
+    y = lighting.diffuse_directional(n, c, ld, lc)
+    _fused_node(y, "DiffuseFn")
+    with pytest.raises(RuntimeError, match="create_graph"):
+        torch.autograd.grad(y.square().sum(), [n], create_graph=True)
+    world, faces = _mesh(8)
+    x = torch.from_numpy(world).to(DEV).requires_grad_(True)
+    nv = lighting.vertex_normals(x, torch.from_numpy(faces).to(DEV))
+    with pytest.raises(RuntimeError, match="create_graph"):
+        torch.autograd.grad(nv.sum(), [x], create_graph=True)
+    # first-order gradients are unaffected
+    g, = torch.autograd.grad(lighting.diffuse_directional(n, c, ld, lc).sum(), [c])
+    assert torch.isfinite(g).all()
+    monkeypatch.setattr(lighting, "_FUSED_ENABLED", False)
+    y2 = lighting.diffuse_directional(n, c, ld, lc)
+    assert "DiffuseFn" not in y2.grad_fn.name()
+    gn, = torch.autograd.grad(y2.square().sum(), [n], create_graph=True)
+    gg, = torch.autograd.grad(gn.sum(), [c])
+    assert torch.isfinite(gg).all()
+
+
 def test_fused_lighting_captures_into_a_graph():
     """No host-to-device copy inside: the fused calls record into a HIP graph and replay to the eager result."""
     world, faces = _mesh(12)

@@ -459,6 +459,33 @@ def test_clip_polygon_vertex_cap():
     check_scene(*scenes.near_w0_scene(seed, W=33, H=17, C=1), seed=seed)
 
 
+def _clip_stats(scene):
+    from dirt_amd.session import RasteriseSession
+    bg, v, c, f = scene
+    if bg.ndim == 3:
+        bg, v, c, f = bg[None], v[None], c[None], f[None]
+    B, H, W, C = bg.shape
+    sess = RasteriseSession(B, H, W, C, v.shape[1], f.shape[1], device="cuda")
+    sess.forward(_gpu(bg), _gpu(v), _gpu(c), _gpu(f))
+    return sess.clip_stats()
+
+
+def test_r5_deviation_counters():
+    """the R5 vertex cap (culls a face a GL driver would keep) and the R5 sub-vertex clamp are
+    counted, so the deviation is measured rather than silent.  Zero on the golden-style scenes and the config-3
+    frame; the cap fires on near_w0 seed 41533, the clamp on fuzz seed 167059."""
+    for name, scene in (("square", scenes.readme_square()), ("cube", scenes.cube_scene()),
+                        ("clipping", scenes.clipping_scene()), ("perspective", scenes.random_triangles(
+                            F=3000, W=200, H=150, perspective=True, seed=3)),
+                        ("c3", scenes.random_triangles(F=50000, W=1024, H=1024, seed=0))):
+        st = _clip_stats(scene)
+        assert st == {"cap_culled": 0, "clamped": 0}, (name, st)
+    st = _clip_stats(scenes.near_w0_scene(41533, W=33, H=17, C=1))
+    assert st["cap_culled"] >= 1, st
+    st = _clip_stats(scenes.fuzz_case(167059))
+    assert st["clamped"] >= 1, st
+
+
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_W0_FUZZ_FIRST", "0")),
                                          int(os.environ.get("DIRT_W0_FUZZ_SEEDS", "8"))))
 def test_fuzz_near_w0_clipping(seed):

@@ -28,6 +28,10 @@ CONFIGS = {
     # forward -- ADVICE r3's large-frame case)
     "c2_cube_4096x4096x3": lambda: [scenes.cube_scene(W=4096, H=4096)],
     "c3_random50k_1024x1024x3": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)],
+    # config 3 frames eight to a launch: the kernels' steady-state time per frame (many workgroup rounds per CU,
+    # so no first-round burst or drain tail in the per-frame figure)
+    "c3x8_random50k_1024x1024x3_batch8": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, seed=b)
+                                                  for b in range(8)],
     "c4_deferred20k_512x512x7": lambda: [scenes.deferred_mesh_scene()],
     "c5_batch8x20k_1024x1024x3_per_gpu": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024, seed=b)
                                                   for b in range(8)],
