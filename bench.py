@@ -373,10 +373,19 @@ def main():
             px = dirt_amd.rasterise_batch(bg_r, v_r, c_r, f)
             torch.autograd.grad(px, [bg_r, v_r, c_r], grad)
 
-        for _ in range(5):
+        # the headline's clock warm-up (the eager op is host-bound, so the GPU idles between launches and its clock
+        # falls back quickly), then at least 200 timed eager steps in chunks of 20: the rate over all of them
+        # plus the median and spread of the chunks (20 steps were noise-dominated)
+        t_w = time.perf_counter()
+        while (time.perf_counter() - t_w) * 1e3 < max(args.min_warm_ms, 50.0):
             api_step()
-        n_api = max(20, args.steps // 2)
-        t_eager = timed(api_step, n_api, barrier, world, device, shared)
+        torch.cuda.synchronize()
+        chunk = 20
+        n_chunks = max(10, -(-args.steps // chunk))
+        chunk_s = [timed(api_step, chunk, barrier, world, device, shared) for _ in range(n_chunks)]
+        n_api = chunk * n_chunks
+        t_eager = sum(chunk_s)
+        rates = sorted(world * B * H * W * chunk / t / 1e6 for t in chunk_s)
         g_api = graph_of(api_step, 1, cap_stream)
         t_graph = timed(g_api.replay, n_api, barrier, world, device, shared)
         del g_api
@@ -391,6 +400,9 @@ def main():
                     "dirt/rasterise_ops.py:57-88), fresh outputs per call, cached scratch",
             "eager_mpix_s": round(world * B * H * W * n_api / t_eager / 1e6, 1),
             "eager_ms_per_step": round(t_eager * 1e3 / n_api, 4),
+            "eager_steps": n_api,
+            "eager_chunks_mpix_s": {"chunk_steps": chunk, "median": round(float(np.median(rates)), 1),
+                                    "min": round(rates[0], 1), "max": round(rates[-1], 1)},
             "graph_mpix_s": round(world * B * H * W * n_api / t_graph / 1e6, 1),
             "graph_ms_per_step": round(t_graph * 1e3 / n_api, 4),
             "graph20_mpix_s": round(world * B * H * W * n20 * 20 / t_graph20 / 1e6, 1),
@@ -579,6 +591,39 @@ def main():
     # ---- leg (N > 1): the output all-gather over RCCL / xGMI, alone and overlapped with the next step
     if world > 1 and not args.no_gather_leg:
         leg("gather", gather_leg)
+
+    def allreduce_leg():
+        """SURVEY 8e's data-parallel fit of one shared mesh (tests/rasterise_tests.py:89): every rank renders its
+        frames and the vertex gradient is summed over the frames and the ranks by one all-reduce per step
+        (sharding.allreduce_shared_gradient, 16 V bytes).  Eager steps with and without the collective."""
+        from dirt_amd.sharding import allreduce_shared_gradient
+        n_s = max(20, args.steps // 2)
+
+        def plain():
+            step()
+
+        def with_ar():
+            step()
+            allreduce_shared_gradient(sess.grad_vertices)
+
+        for _ in range(3):
+            with_ar()
+        torch.cuda.synchronize()
+        t_plain = timed(plain, n_s, barrier, world, device, shared)
+        t_ar = timed(with_ar, n_s, barrier, world, device, shared)
+        t_only = timed(lambda: allreduce_shared_gradient(sess.grad_vertices), n_s, barrier, world, device, shared)
+        legs["shared_allreduce"] = {
+            "what": "fwd+bwd per rank + one all-reduce of the shared vertex gradient [V,4] over %s per step "
+                    "(eager steps)" % ("gloo (shared-GPU rehearsal)" if shared else "RCCL / xGMI"),
+            "allreduce_bytes": V * 4 * 4,
+            "allreduce_ms": round(t_only * 1e3 / n_s, 4),
+            "value_eager_without": round(world * B * H * W * n_s / t_plain / 1e6, 1),
+            "value_with_allreduce": round(world * B * H * W * n_s / t_ar / 1e6, 1),
+            "ms_per_step_with_allreduce": round(t_ar * 1e3 / n_s, 4)}
+
+    # ---- leg (N > 1): the shared-parameter gradient all-reduce of a data-parallel pose fit
+    if world > 1 and not args.no_gather_leg:
+        leg("shared_allreduce", allreduce_leg)
 
     cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

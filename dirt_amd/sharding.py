@@ -143,6 +143,19 @@ def shared_across_ranks(x, group=None):
     return _SharedGradAllReduce.apply(x, group)
 
 
+def allreduce_shared_gradient(grad, group=None, async_op=False):
+    """The collective of a data-parallel fit of one shared mesh (tests/rasterise_tests.py:89 tiles one mesh
+    over the batch): this rank's per-frame gradient `grad` [b_local, ...] (e.g. RasteriseSession's
+    grad_vertices) is summed over its frames, then over the ranks with one all-reduce (RCCL over xGMI with the
+    "nccl" backend).  Returns the batch's gradient [...] on every rank (and the work handle if async_op).
+    The same sum shared_across_ranks produces inside autograd, for callers that drive the op without it."""
+    total = grad.sum(0) if grad.dim() > 0 and grad.shape[0] != 1 else grad.reshape(grad.shape[1:]).clone()
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return (total, None) if async_op else total
+    work = dist.all_reduce(total, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return (total, work) if async_op else total
+
+
 def rasterise_batch_sharded(background, vertices, vertex_colors, faces, camera_pos=None, height=None, width=None,
                             channels=None, group=None, gather=False, render=rasterise_batch, gather_dtype=None):
     """rasterise_batch over this rank's contiguous share of the frames.

@@ -14,8 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import scenes
-from dirt_amd.sharding import (gather_frames, gather_frames_async, gather_frames_to, gather_frames_to_async,
-                               rasterise_batch_sharded, shard_bounds, shared_across_ranks)
+from dirt_amd.sharding import (allreduce_shared_gradient, gather_frames, gather_frames_async, gather_frames_to,
+                               gather_frames_to_async, rasterise_batch_sharded, shard_bounds, shared_across_ranks)
 from oracle import oracle
 
 
@@ -71,6 +71,15 @@ def _worker(rank, world, port, inputs, outq):
         x = torch.arange(6, dtype=torch.float32).requires_grad_(True)
         loss = (shared_across_ranks(x) * (rank + 1)).sum() + (x * x).sum() * 0.0
         loss.backward()
+        # bench.py's legs.shared_allreduce collective: per-frame gradients of this rank's frames, summed over
+        # the frames and then the ranks (frame k's gradient is k + 1 everywhere, so the batch sum is known)
+        per_frame = torch.stack([torch.full((7, 4), float(k + 1)) for k in range(lo, hi)]) if hi > lo else \
+            torch.zeros((0, 7, 4))
+        total = allreduce_shared_gradient(per_frame) if hi - lo != 0 else None
+        t2, work = allreduce_shared_gradient(per_frame, async_op=True) if hi - lo != 0 else (None, None)
+        if work is not None:
+            work.wait()
+        red["allreduce"] = (None if total is None else total.numpy(), None if t2 is None else t2.numpy())
         outq.put((rank, lo, hi, local.numpy(), full.numpy(), full2.numpy(), full3.numpy(), x.grad.numpy(), root, red))
     finally:
         dist.destroy_process_group()
@@ -93,6 +102,9 @@ def test_two_rank_sharded_batch_matches_single_process(B):
     res.sort(key=lambda r: r[0])
     covered = []
     for rank, lo, hi, local, full, full2, full3, xgrad, root, red in res:
+        want_sum = np.full((7, 4), B * (B + 1) / 2, np.float32)  # sum over the batch's frames of (k + 1)
+        for got in red["allreduce"]:
+            np.testing.assert_array_equal(got, want_sum)
         for dt in (torch.bfloat16, torch.float16):
             want = torch.from_numpy(ref).to(dt).float().numpy()
             for k, got in enumerate(red[str(dt)]):
