@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 #include <string>
@@ -193,6 +194,7 @@ int validate(int B, int H, int W, int C, int V, int F)
 #include "setup_kernel.h"
 #include "raster_kernel.h"
 #include "grad_kernel.h"
+#include "grad_persist.h"
 #include "lighting_kernels.h"
 
 // zero two float arrays in one launch (the backward's atomically accumulated outputs)
@@ -431,6 +433,30 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
                               bin_capacity, 0u, nullptr, nullptr, stream_);
 }
 
+// compute units of the current device (cached per device)
+static int device_cus()
+{
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int n = 0;
+        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cache[dev];
+}
+
+// DIRT_GRAD_PERSIST: workgroups per CU of the persistent backward (0 / unset = the one-tile-per-workgroup grid)
+static int grad_persist_wgs_per_cu()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("DIRT_GRAD_PERSIST");
+        v = e ? std::max(0, atoi(e)) : 0;
+    }
+    return v;
+}
+
 static NdcScale ndc_scale(int W, int H)
 {
     return NdcScale{2.0f / (float)W, 2.0f / (float)H, 0.5f * (float)W, 0.5f * (float)H};
@@ -476,6 +502,19 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(C) - 1) / grad_tile_h(C);
     dim3 grid((unsigned)(gntx * gnty), (unsigned)B);
     ProfScope ps(K_GRAD, stream);
+    // persistent backward (grad_kernel PERSIST): workgroups per CU from DIRT_GRAD_PERSIST (0 = off), RGB with both
+    // gradients, when the batch has more tiles than that many workgroups
+    const int64_t gtiles = (int64_t)gntx * gnty * B;
+    const int pwpc = grad_persist_wgs_per_cu();
+    if (pwpc > 0 && C == 3 && gm == 3 && kGradTileW == 16 && gtiles > (int64_t)pwpc * device_cus()) {
+        const unsigned nwg = (unsigned)std::min<int64_t>(gtiles, (int64_t)pwpc * device_cus());
+        grad_kernel_persist<3, 0, kGradTileW, grad_tile_h(3), 3><<<dim3(nwg), dim3(GradGeom<kGradTileW, grad_tile_h(3)>::NT),
+                                                                0, stream>>>(
+            pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,
+            grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H), gntx * gnty);
+        HIP_TRY(hipGetLastError());
+        return DIRT_OK;
+    }
 #define LAUNCH_GRAD_GM(CC, GMV)                                                                              \
     grad_kernel<CC, 0, kGradTileW, grad_tile_h(CC), GMV><<<grid, dim3(GradGeom<kGradTileW, grad_tile_h(CC)>::NT), 0, \
                                                           stream>>>(                                            \
