@@ -415,54 +415,65 @@ def main():
         leg("api_autograd", api_leg)
 
     def recompute_leg():
-        """The single-output op's gradient (dirt_rasterise_bwd_recompute): forward + recompute backward per
-        step, graph-captured like the headline step, against the stateful session step."""
+        """The single-output op (dirt_rasterise_fwd_stash + the registered gradient dirt_rasterise_bwd_recompute on
+        the op's workspace), graph-captured like the headline step, against the stateful session step; and the
+        same gradient when the workspace does not hold the geometry (always recomputed: setup + bins +
+        coverage-only raster + backward kernel)."""
         lib = _lib.load()
         n_ws = _lib.recompute_workspace_size(B, H, W, C, V, F)
         ws = torch.zeros((n_ws,), dtype=torch.uint8, device=device)
+        ws2 = torch.zeros((n_ws,), dtype=torch.uint8, device=device)
+        px = torch.empty((B, H, W, C), device=device)
         gv = torch.empty((B, V, 4), device=device)
         gc = torch.empty((B, V, C), device=device)
         gbg = torch.empty((B, H, W, C), device=device)
 
-        def rc_bwd():
+        def rc_bwd(w, flags, pixels=px):
             stream = torch.cuda.current_stream(device).cuda_stream
             _lib.check(lib.dirt_rasterise_bwd_recompute(
-                bg.data_ptr(), v.data_ptr(), c.data_ptr(), f.data_ptr(), sess.pixels.data_ptr(), grad.data_ptr(),
-                B, H, W, C, V, F, gv.data_ptr(), gc.data_ptr(), gbg.data_ptr(), ws.data_ptr(), n_ws,
-                _lib.BWD_SCRATCH_CLEAN, stream))
+                bg.data_ptr(), v.data_ptr(), c.data_ptr(), f.data_ptr(), pixels.data_ptr(), grad.data_ptr(),
+                B, H, W, C, V, F, gv.data_ptr(), gc.data_ptr(), gbg.data_ptr(), w.data_ptr(), n_ws, flags, stream))
 
-        def rc_step():
+        def stash_step():
+            stream = torch.cuda.current_stream(device).cuda_stream
+            _lib.check(lib.dirt_rasterise_fwd_stash(bg.data_ptr(), v.data_ptr(), c.data_ptr(), f.data_ptr(), B, H, W,
+                                                    C, V, F, px.data_ptr(), ws.data_ptr(), n_ws,
+                                                    _lib.FWD_SCRATCH_CLEAN, stream))
+            rc_bwd(ws, _lib.BWD_SCRATCH_CLEAN)
+
+        def miss_step():
+            # (flags 0: the workspace is not vouched clean, so its stash header is reset -- always a recomputation)
             sess.forward(bg, v, c, f)
-            rc_bwd()
+            rc_bwd(ws2, 0, sess.pixels)
 
-        for _ in range(5):
-            rc_step()
-        n_rc = max(20, args.steps)
-        g_rc = graph_of(rc_step, min(n_rc, 200), cap_stream) if not args.no_graph else None
-        reps = max(1, n_rc // min(n_rc, 200)) if g_rc else n_rc
-        t_rc = timed(g_rc.replay if g_rc else rc_step, reps, barrier, world, device, shared)
-        steps_rc = reps * (min(n_rc, 200) if g_rc else 1)
-        kr = kernel_times(rc_bwd, args.profile_steps)
-        g_b = graph_of(rc_bwd, 50, cap_stream) if not args.no_graph else None
-        bwd_graph_us = None
-        if g_b is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            g_b.replay()
-            e1.record()
-            torch.cuda.synchronize()
-            bwd_graph_us = round(e0.elapsed_time(e1) * 1e3 / 50, 2)
+        out = {}
+        for name, fn in (("stash", stash_step), ("no_stash", miss_step)):
+            for _ in range(5):
+                fn()
+            n_rc = max(20, args.steps)
+            g_rc = graph_of(fn, min(n_rc, 200), cap_stream) if not args.no_graph else None
+            reps = max(1, n_rc // min(n_rc, 200)) if g_rc else n_rc
+            t_rc = timed(g_rc.replay if g_rc else fn, reps, barrier, world, device, shared)
+            steps_rc = reps * (min(n_rc, 200) if g_rc else 1)
+            out[name] = (t_rc, steps_rc)
+            del g_rc
+        st = _lib.stash_state(B, H, W, C, V, F, ws.data_ptr(), n_ws, torch.cuda.current_stream(device).cuda_stream)
+        kr = kernel_times(lambda: rc_bwd(ws, _lib.BWD_SCRATCH_CLEAN), args.profile_steps)
+        (t_s, n_s), (t_m, n_m) = out["stash"], out["no_stash"]
         legs["recompute_bwd"] = {
-            "what": "forward + dirt_rasterise_bwd_recompute per step (the single-output op's registered gradient: "
-                    "setup + bins + coverage-only raster + backward kernel from the op's inputs, output and "
-                    "grad_pixels), workspace zero-filled once",
-            "mpix_s": round(world * B * H * W * steps_rc / t_rc / 1e6, 1),
-            "ms_per_step": round(t_rc * 1e3 / steps_rc, 4),
+            "what": "the single-output op per step: dirt_rasterise_fwd_stash + its registered gradient "
+                    "dirt_rasterise_bwd_recompute on the op's workspace (the geometry compared bitwise on the device; "
+                    "unchanged, so the recomputation is skipped); no_stash: the same gradient recomputing setup + "
+                    "bins + coverage-only raster every step",
+            "mpix_s": round(world * B * H * W * n_s / t_s / 1e6, 1),
+            "ms_per_step": round(t_s * 1e3 / n_s, 4),
             "stateful_ms_per_step": round(ms_per_step, 4),
-            "extra_us_per_step": round((t_rc / steps_rc - ms_per_step * 1e-3) * 1e6, 2),
-            "bwd_kernels_us": {k: round(u, 2) for k, u in kr.items()},
-            "bwd_graph_us": bwd_graph_us}
-        del g_rc, g_b, ws
+            "extra_us_per_step": round((t_s / n_s - ms_per_step * 1e-3) * 1e6, 2),
+            "stash_last_missed": st["last_missed"],
+            "no_stash_mpix_s": round(world * B * H * W * n_m / t_m / 1e6, 1),
+            "no_stash_extra_us_per_step": round((t_m / n_m - ms_per_step * 1e-3) * 1e6, 2),
+            "bwd_kernels_us": {k: round(u, 2) for k, u in kr.items()}}
+        del ws, ws2
         step()
         torch.cuda.synchronize()
 

@@ -27,7 +27,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes
@@ -52,6 +52,7 @@ SIGNATURES = {
     "dirt_bwd_recompute_workspace_size": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(_SZ)]),
     "dirt_rasterise_bwd_recompute": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _U,
                                           _P]),
+    "dirt_rasterise_fwd_stash": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _U, _P]),
     "dirt_scratch_clear": (_I, [_I, _I, _I, _I, _I64, _P, _SZ, _P]),
     "dirt_check_faces": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
     "dirt_stream_capture_id": (_I, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
@@ -142,6 +143,18 @@ def clip_stats(B, H, W, F, bin_capacity, scratch, scratch_bytes, stream, reset=T
     check(fn(B, H, W, F, bin_capacity, scratch, scratch_bytes, stream, 1 if reset else 0, ctypes.byref(cap),
              ctypes.byref(clamped)))
     return {"cap_culled": cap.value, "clamped": clamped.value}
+
+
+def stash_state(B, H, W, C, V, F, workspace, workspace_bytes, stream):
+    """Debug (synchronises `stream`): {"last_missed": 1 if the last dirt_rasterise_bwd_recompute on this workspace
+    recomputed, 0 if it reused the gradient stash; "magic": the stash header's magic word (0 = never written)}."""
+    lib = load()
+    fn = lib.dirt_debug_stash_state
+    fn.restype = ctypes.c_int
+    fn.argtypes = [_I] * 6 + [_P, _SZ, _P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    miss, magic = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    check(fn(B, H, W, C, V, F, workspace, workspace_bytes, stream, ctypes.byref(miss), ctypes.byref(magic)))
+    return {"last_missed": miss.value, "magic": magic.value}
 
 
 NUM_KERNELS = 3

@@ -240,6 +240,68 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
         if (faces[k] < 0 || faces[k] >= V) atomicOr(flag, 1u);
 }
 
+// ---- gradient stash of the single-output op (header words: setup_kernel.h kStash*)
+struct StashDims {
+    uint32_t d[5];  // B, H, W, V, F
+};
+
+// words of a and b equal?  (16-B loads when both are 16-B aligned, the tail and misaligned buffers by words)
+__device__ __forceinline__ bool words_differ(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b, int64_t n,
+                                             int64_t gid, int64_t gs)
+{
+    bool diff = false;
+    const bool vec = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+    const int64_t n4 = vec ? n / 4 : 0;
+    for (int64_t k = gid; k < n4; k += gs) {
+        const uint4 x = reinterpret_cast<const uint4 *>(a)[k], y = reinterpret_cast<const uint4 *>(b)[k];
+        diff = diff || x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+    }
+    for (int64_t k = 4 * n4 + gid; k < n; k += gs) diff = diff || a[k] != b[k];
+    return diff;
+}
+
+// Does the workspace hold the records of exactly this geometry?  Bitwise comparison of vertices and faces with the
+// copies the last forward-stash or recompute left (the records, g-buffer and coverage bits are a deterministic
+// function of those bits and the frame size), plus the header's magic and dims.  Any difference sets this call's
+// miss flag; the next call's flag is zeroed here (nothing reads it in this call).
+__global__ __launch_bounds__(256) void stash_check_kernel(const uint32_t *__restrict__ v, const uint32_t *__restrict__ vt,
+                                                          int64_t nv, const uint32_t *__restrict__ f,
+                                                          const uint32_t *__restrict__ ft, int64_t nf, uint32_t *hdr,
+                                                          StashDims dims)
+{
+    const uint32_t p = hdr[kStashP] & 1u;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+    bool miss = words_differ(v, vt, nv, gid, gs) || words_differ(f, ft, nf, gid, gs);
+    if (gid == 0) {
+        hdr[kStashMiss + 16 * (p ^ 1u)] = 0u;
+        miss = miss || hdr[kStashMagicW] != kStashMagic;
+        for (int k = 0; k < 5; ++k) miss = miss || hdr[kStashDims + k] != dims.d[k];
+    }
+    if (__ballot(miss) != 0 && (threadIdx.x & 63) == 0) atomicOr(&hdr[kStashMiss + 16 * p], 1u);
+}
+
+__global__ void stash_flip_kernel(uint32_t *p)
+{
+    if (threadIdx.x == 0) p[0] ^= 1u;
+}
+
+// After a recomputation (this call's miss flag set), or unconditionally for a forward-stash (`force`): record the
+// geometry the workspace now holds.
+__global__ __launch_bounds__(256) void stash_update_kernel(const uint32_t *__restrict__ v, uint32_t *__restrict__ vt,
+                                                           int64_t nv, const uint32_t *__restrict__ f,
+                                                           uint32_t *__restrict__ ft, int64_t nf, uint32_t *hdr,
+                                                           StashDims dims, int force)
+{
+    if (!force && stash_hit(hdr)) return;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = gid; k < nv; k += gs) vt[k] = v[k];
+    for (int64_t k = gid; k < nf; k += gs) ft[k] = f[k];
+    if (gid == 0) {
+        hdr[kStashMagicW] = kStashMagic;
+        for (int k = 0; k < 5; ++k) hdr[kStashDims + k] = dims.d[k];
+    }
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -247,7 +309,7 @@ __global__ void check_faces_kernel(const int32_t *__restrict__ faces, int64_t n,
 
 extern "C" {
 
-int dirt_abi_version(void) { return 10; }
+int dirt_abi_version(void) { return 11; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -272,7 +334,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
                               int shader_id, float *pixels, int32_t *gbuffer, void *saved, size_t saved_bytes,
                               void *scratch, size_t scratch_bytes, int64_t bin_capacity, unsigned flags,
                               float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream_,
-                              GbufOut gbo = GbufOut{}, bool nopix = false)
+                              GbufOut gbo = GbufOut{}, bool nopix = false, const uint32_t *stash_hdr = nullptr)
 {
     int rc = validate(B, H, W, C, V, F);
     if (rc) return rc;
@@ -319,7 +381,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     if (F > 0 && !fused) {
         ProfScope ps(K_SETUP, stream);
         launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream, zero_grad_vertices,
-                        (int64_t)B * V * 4, zero_grad_vertex_colors, (int64_t)B * V * C);
+                        (int64_t)B * V * 4, zero_grad_vertex_colors, (int64_t)B * V * C, stash_hdr);
         HIP_TRY(hipGetLastError());
         // (the setup grid's filler workgroups zero the accumulators; the raster does it only when F == 0)
         zero_grad_vertices = nullptr;
@@ -346,13 +408,15 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
             L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
             zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
-            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo, faces);   \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo, faces,    \
+            stash_hdr);                                                                                          \
     else if (nopix)                                                                                              \
         raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, false, false, true><<<grid, dim3(256), 0, stream>>>(           \
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
             L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
             zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
-            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo);          \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, gbo, nullptr,  \
+            stash_hdr);                                                                                          \
     else if (deep && !fused && !want_gb)                                                                         \
         raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, false, false, false, true><<<grid, dim3(256), 0, stream>>>(     \
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
@@ -462,10 +526,13 @@ static NdcScale ndc_scale(int W, int H)
     return NdcScale{2.0f / (float)W, 2.0f / (float)H, 0.5f * (float)W, 0.5f * (float)H};
 }
 
-int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces, const float *pixels,
-                       const float *grad_pixels, const int32_t *gbuffer, const void *saved, int B, int H, int W, int C,
-                       int V, int F, float *grad_vertices, float *grad_vertex_colors, float *grad_background,
-                       unsigned flags, void *stream_)
+}  // extern "C"
+
+// the backward of dirt_rasterise_bwd; stash_flip: the recompute workspace's stash parity (flipped by the launch)
+static int rasterise_bwd_impl(const float *vertices, const float *vertex_colors, const int32_t *faces,
+                              const float *pixels, const float *grad_pixels, const int32_t *gbuffer, const void *saved,
+                              int B, int H, int W, int C, int V, int F, float *grad_vertices, float *grad_vertex_colors,
+                              float *grad_background, unsigned flags, void *stream_, uint32_t *stash_flip)
 {
     // vertices / vertex_colors / faces are part of the contract (rasterise_grad_common.h:19-24); the
     // forward's FaceData in `saved` already holds what the kernel needs from them.
@@ -496,7 +563,13 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     if (gm == 0) {
         // V == 0 (no vertex or colour gradient exists): the launch still writes grad_background; the colour
         // path's instantiation with a null colour pointer has nothing to flush (every pixel is background)
-        if (!grad_background) return DIRT_OK;
+        if (!grad_background) {
+            if (stash_flip) {  // (no grad launch to flip the stash parity)
+                stash_flip_kernel<<<dim3(1), dim3(64), 0, stream>>>(stash_flip);
+                HIP_TRY(hipGetLastError());
+            }
+            return DIRT_OK;
+        }
     }
     // backward tiles: kGradTileW x grad_tile_h(C) (grad_kernel.h)
     const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(C) - 1) / grad_tile_h(C);
@@ -511,7 +584,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
         grad_kernel_persist<3, 0, kGradTileW, grad_tile_h(3), 3><<<dim3(nwg), dim3(GradGeom<kGradTileW, grad_tile_h(3)>::NT),
                                                                 0, stream>>>(
             pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,
-            grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H), gntx * gnty);
+            grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H), gntx * gnty, stash_flip);
         HIP_TRY(hipGetLastError());
         return DIRT_OK;
     }
@@ -519,7 +592,7 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     grad_kernel<CC, 0, kGradTileW, grad_tile_h(CC), GMV><<<grid, dim3(GradGeom<kGradTileW, grad_tile_h(CC)>::NT), 0, \
                                                           stream>>>(                                            \
         pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,          \
-        grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H))
+        grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H), stash_flip)
 #define LAUNCH_GRAD(CC)                                                                                       \
     do {                                                                                                      \
         if (gm == 1) LAUNCH_GRAD_GM(CC, 1);                                                                   \
@@ -536,12 +609,54 @@ int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const 
     return DIRT_OK;
 }
 
-// Workspace of the recompute backward: [saved | scratch | g-buffer], each 256-B aligned
-static void recompute_parts(const Layout &L, int B, int H, int W, size_t &off_scratch, size_t &off_gbuf, size_t &total)
+extern "C" {
+
+int dirt_rasterise_bwd(const float *vertices, const float *vertex_colors, const int32_t *faces, const float *pixels,
+                       const float *grad_pixels, const int32_t *gbuffer, const void *saved, int B, int H, int W, int C,
+                       int V, int F, float *grad_vertices, float *grad_vertex_colors, float *grad_background,
+                       unsigned flags, void *stream_)
 {
-    off_scratch = (size_t)align_up((int64_t)L.saved_total, 256);
-    off_gbuf = off_scratch + (size_t)align_up((int64_t)L.scratch_total, 256);
-    total = off_gbuf + (size_t)align_up((int64_t)B * H * W * 4, 256);
+    return rasterise_bwd_impl(vertices, vertex_colors, faces, pixels, grad_pixels, gbuffer, saved, B, H, W, C, V, F,
+                              grad_vertices, grad_vertex_colors, grad_background, flags, stream_, nullptr);
+}
+
+// Workspace of the recompute backward: [saved | scratch | g-buffer | stash header | vertex copy | face copy], each
+// 256-B aligned.  The stash (ABI v11): the geometry (vertices, faces, bitwise) whose records, g-buffer and coverage
+// bits the workspace holds, written by dirt_rasterise_fwd_stash or after a recomputation.
+struct RecomputeParts {
+    size_t off_scratch, off_gbuf, off_hdr, off_vtag, off_ftag, total;
+};
+static RecomputeParts recompute_parts(const Layout &L, int B, int H, int W, int V, int F)
+{
+    RecomputeParts P;
+    P.off_scratch = (size_t)align_up((int64_t)L.saved_total, 256);
+    P.off_gbuf = P.off_scratch + (size_t)align_up((int64_t)L.scratch_total, 256);
+    P.off_hdr = P.off_gbuf + (size_t)align_up((int64_t)B * H * W * 4, 256);
+    P.off_vtag = P.off_hdr + 256;
+    P.off_ftag = P.off_vtag + (size_t)align_up((int64_t)B * V * 16, 256);
+    P.total = P.off_ftag + (size_t)align_up((int64_t)B * F * 12, 256);
+    return P;
+}
+
+// launch the stash check (check = true) or update of a recompute workspace for this geometry
+static int launch_stash(bool check, bool force, const float *vertices, const int32_t *faces, int B, int H, int W,
+                        int V, int F, char *ws, const RecomputeParts &P, hipStream_t stream)
+{
+    const int64_t nv = (int64_t)B * V * 4, nf = (int64_t)B * F * 3;
+    const StashDims dims{{(uint32_t)B, (uint32_t)H, (uint32_t)W, (uint32_t)V, (uint32_t)F}};
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(ws + P.off_hdr);
+    uint32_t *vt = reinterpret_cast<uint32_t *>(ws + P.off_vtag), *ft = reinterpret_cast<uint32_t *>(ws + P.off_ftag);
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, (std::max(nv / 4, nf) + 255) / 256));
+    if (check)
+        stash_check_kernel<<<dim3(blocks), dim3(256), 0, stream>>>(reinterpret_cast<const uint32_t *>(vertices), vt, nv,
+                                                                   reinterpret_cast<const uint32_t *>(faces), ft, nf,
+                                                                   hdr, dims);
+    else
+        stash_update_kernel<<<dim3(blocks), dim3(256), 0, stream>>>(reinterpret_cast<const uint32_t *>(vertices), vt,
+                                                                    nv, reinterpret_cast<const uint32_t *>(faces), ft,
+                                                                    nf, hdr, dims, force ? 1 : 0);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
 }
 
 int dirt_bwd_recompute_workspace_size(int B, int H, int W, int C, int V, int F, size_t *workspace_bytes)
@@ -551,9 +666,7 @@ int dirt_bwd_recompute_workspace_size(int B, int H, int W, int C, int V, int F, 
     Layout L;
     rc = make_layout(B, H, W, F, 0, L);
     if (rc) return rc;
-    size_t os, og, tot;
-    recompute_parts(L, B, H, W, os, og, tot);
-    if (workspace_bytes) *workspace_bytes = tot;
+    if (workspace_bytes) *workspace_bytes = recompute_parts(L, B, H, W, V, F).total;
     return DIRT_OK;
 }
 
@@ -578,23 +691,63 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
     Layout L;
     rc = make_layout(B, H, W, F, 0, L);
     if (rc) return rc;
-    size_t os, og, tot;
-    recompute_parts(L, B, H, W, os, og, tot);
-    if (workspace_bytes < tot)
+    const RecomputeParts P = recompute_parts(L, B, H, W, V, F);
+    if (workspace_bytes < P.total)
         return fail(DIRT_EINVAL, "RasteriseGrad: workspace smaller than dirt_bwd_recompute_workspace_size()");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     char *ws = static_cast<char *>(workspace);
-    int32_t *gbuf = reinterpret_cast<int32_t *>(ws + og);
+    int32_t *gbuf = reinterpret_cast<int32_t *>(ws + P.off_gbuf);
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(ws + P.off_hdr);
     const bool acc = (flags & DIRT_BWD_ACCUMULATE) != 0;
+    const bool clean = (flags & DIRT_BWD_SCRATCH_CLEAN) != 0;
+    // (a workspace not vouched clean starts from scratch: bin counters and the stash header zeroed -- a miss)
+    if (!clean) HIP_TRY(hipMemsetAsync(hdr, 0, 256, stream));
+    // stash check: does the workspace already hold this geometry's records, g-buffer and coverage bits (left by
+    // dirt_rasterise_fwd_stash or by the previous recomputation)?  The recomputation below then exits at once
+    // (device-side; the setup's filler workgroups still zero the accumulators).
+    rc = launch_stash(true, false, vertices, faces, B, H, W, V, F, ws, P, stream);
+    if (rc) return rc;
     // the recomputation zero-fills the gradient accumulators in passing (setup filler workgroups), so the
     // backward below only adds into them
     rc = rasterise_fwd_impl(nullptr, C, vertices, nullptr, faces, nullptr, B, H, W, C, V, F, DIRT_SHADER_GOURAUD,
-                            nullptr, gbuf, ws, L.saved_total, ws + os, L.scratch_total, 0,
-                            (flags & DIRT_BWD_SCRATCH_CLEAN) ? DIRT_FWD_SCRATCH_CLEAN : 0u,
-                            acc ? nullptr : grad_vertices, acc ? nullptr : grad_vertex_colors, stream_, GbufOut{},
-                            /*nopix=*/true);
+                            nullptr, gbuf, ws, L.saved_total, ws + P.off_scratch, L.scratch_total, 0,
+                            clean ? DIRT_FWD_SCRATCH_CLEAN : 0u, acc ? nullptr : grad_vertices,
+                            acc ? nullptr : grad_vertex_colors, stream_, GbufOut{}, /*nopix=*/true, hdr);
     if (rc) return rc;
-    return dirt_rasterise_bwd(vertices, vertex_colors, faces, pixels, grad_pixels, gbuf, ws, B, H, W, C, V, F,
-                              grad_vertices, grad_vertex_colors, grad_background, DIRT_BWD_ACCUMULATE, stream_);
+    // after a recomputation the workspace holds this geometry: record it for the next call
+    rc = launch_stash(false, false, vertices, faces, B, H, W, V, F, ws, P, stream);
+    if (rc) return rc;
+    return rasterise_bwd_impl(vertices, vertex_colors, faces, pixels, grad_pixels, gbuf, ws, B, H, W, C, V, F,
+                              grad_vertices, grad_vertex_colors, grad_background, DIRT_BWD_ACCUMULATE, stream_, hdr);
+}
+
+// The single-output op's forward with its gradient stash: dirt_rasterise_fwd (Gouraud) whose records, g-buffer and
+// coverage bits go into a recompute workspace, which then also records the geometry; a dirt_rasterise_bwd_recompute
+// with that workspace and bitwise the same vertices and faces skips its recomputation.
+int dirt_rasterise_fwd_stash(const float *background, const float *vertices, const float *vertex_colors,
+                             const int32_t *faces, int B, int H, int W, int C, int V, int F, float *pixels,
+                             void *workspace, size_t workspace_bytes, unsigned flags, void *stream_)
+{
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    if (B == 0) return DIRT_OK;
+    if (!workspace) return fail(DIRT_EINVAL, "Rasterise: null workspace");
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    const RecomputeParts P = recompute_parts(L, B, H, W, V, F);
+    if (workspace_bytes < P.total)
+        return fail(DIRT_EINVAL, "Rasterise: workspace smaller than dirt_bwd_recompute_workspace_size()");
+    char *ws = static_cast<char *>(workspace);
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const bool clean = (flags & DIRT_FWD_SCRATCH_CLEAN) != 0;
+    if (!clean) HIP_TRY(hipMemsetAsync(ws + P.off_hdr, 0, 256, stream));
+    rc = rasterise_fwd_impl(background, C, vertices, vertex_colors, faces, nullptr, B, H, W, C, V, F,
+                            DIRT_SHADER_GOURAUD, pixels, reinterpret_cast<int32_t *>(ws + P.off_gbuf), ws,
+                            L.saved_total, ws + P.off_scratch, L.scratch_total, 0, clean ? DIRT_FWD_SCRATCH_CLEAN : 0u,
+                            nullptr, nullptr, stream_);
+    if (rc) return rc;
+    return launch_stash(false, true, vertices, faces, B, H, W, V, F, ws, P, stream);
 }
 
 __global__ void bin_occupancy_kernel(const uint32_t *__restrict__ counts, int64_t nslabs, uint32_t slab, uint32_t *out)
@@ -659,6 +812,29 @@ int dirt_debug_clip_stats(int B, int H, int W, int F, int64_t bin_capacity, void
     HIP_TRY(hipStreamSynchronize(stream));
     if (cap_culled) *cap_culled = h[0];
     if (clamped) *clamped = h[1];
+    return DIRT_OK;
+}
+
+// Debug (synchronises `stream`): whether the last dirt_rasterise_bwd_recompute on `workspace` recomputed (1: the
+// stash did not hold its geometry) or reused the stash (0), and the header's magic word.  Not part of
+// include/dirt_mi355x.h.
+int dirt_debug_stash_state(int B, int H, int W, int C, int V, int F, const void *workspace, size_t workspace_bytes,
+                           void *stream_, uint32_t *last_missed, uint32_t *magic)
+{
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    const RecomputeParts P = recompute_parts(L, B, H, W, V, F);
+    if (!workspace || workspace_bytes < P.total) return fail(DIRT_EINVAL, "dirt_debug_stash_state: workspace too small");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    uint32_t h[64];
+    HIP_TRY(hipMemcpyAsync(h, static_cast<const char *>(workspace) + P.off_hdr, 256, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const uint32_t p = h[kStashP] & 1u;  // (the last call's grad launch flipped it: that call used p ^ 1)
+    if (last_missed) *last_missed = h[kStashMiss + 16 * (p ^ 1u)];
+    if (magic) *magic = h[kStashMagicW];
     return DIRT_OK;
 }
 

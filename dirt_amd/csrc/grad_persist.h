@@ -23,8 +23,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
                                                    const FaceData *__restrict__ fdata, int B, int H, int W, int Cdyn,
                                                    int V, int F, TileGrid tg, int64_t nrec, float *__restrict__ grad_verts,
                                                    float *__restrict__ grad_colors, float *__restrict__ grad_bg,
-                                                   const NdcScale ns, int ntiles_frame = 0)
-{
+                                                   const NdcScale ns, int ntiles_frame = 0,
+                                                   uint32_t *__restrict__ stash_flip = nullptr)
+{    // recompute backward: flip the gradient stash's parity for the next call (dirt_raster.hip stash_check_kernel)
+    if (stash_flip != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stash_flip[0] ^= 1u;
+
     constexpr int CM = CC > 0 ? CC : DIRT_MAX_CHANNELS;
     constexpr int NT = GradGeom<TWX, TH>::NT, kHalo = GradGeom<TWX, TH>::HX, kHaloPix = GradGeom<TWX, TH>::PIX;
     // LDS pixel stride: float4 for RGB, two float4 for 5..8 channels (wide LDS reads)

@@ -527,7 +527,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      int64_t nzero_a, float *__restrict__ zero_b, int64_t nzero_b,
                                                      const float *__restrict__ verts, const float *__restrict__ cam,
                                                      int sid, int tcb, GbufOut gbo = GbufOut{},
-                                                     const int32_t *__restrict__ faces = nullptr)
+                                                     const int32_t *__restrict__ faces = nullptr,
+                                                     const uint32_t *__restrict__ stash_hdr = nullptr)
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     static_assert(!(GB && kNoDepth), "hill has no depth buffer");
@@ -654,6 +655,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             for (int64_t k = 4 * n4 + gt; k < nzero_b; k += gs) zero_b[k] = 0.f;
         }
     }
+    // the recompute backward's coverage pass: nothing more to do on a stash hit (the workspace already holds this
+    // geometry's g-buffer and coverage bits; the Q parity above republished the value it had, setup having skipped)
+    if (NOPIX && stash_hdr != nullptr && stash_hit(stash_hdr)) return;
     // an overflowed slab (more pairs than its capacity): filter every record of the frame instead
     const bool overflow = FUSED || raw > slab;
     const uint32_t n_items = overflow ? (uint32_t)nrec : raw;

@@ -31,6 +31,18 @@ static_assert(kMaxClipVerts - 2 == kExtraPerFace + 1, "sub-triangle slots");
 // from the reference's for reasons other than driver arithmetic.  Only the clipping slow path touches them.
 constexpr int kStatCapCulled = 48, kStatClamped = 52;
 
+// Gradient stash of the single-output op (dirt_rasterise_fwd_stash / dirt_rasterise_bwd_recompute): a 256-B header
+// in the recompute workspace.  Words: kStashP parity p; kStashMiss + 16 p the current call's miss flag (set by
+// stash_check_kernel when the workspace does not hold this geometry), the other one zeroed by the same check for the
+// next call; the backward's grad launch flips p.  Between calls the current flag is 0 (zeroed workspace: p = 0).
+constexpr int kStashP = 0, kStashMiss = 16, kStashMagicW = 48, kStashDims = 49;  // dims: B, H, W, V, F
+constexpr uint32_t kStashMagic = 0xD1275A5Eu;
+__device__ __forceinline__ bool stash_hit(const uint32_t *hdr)
+{
+    const uint32_t p = hdr[kStashP] & 1u;
+    return hdr[kStashMiss + 16 * p] == 0u;
+}
+
 // R5 slow path: clip against z>=-w and the guard planes, fan-triangulate, write the sub-records.
 // Not inlined so that its stack arrays do not inflate the fast path.  Returns nsub.  `flag`: the scratch's
 // flag area (the R5 deviation counters above), may be null.
@@ -284,7 +296,8 @@ __global__ __launch_bounds__(NT) void setup_kernel(const float *__restrict__ ver
                                                             Rec *__restrict__ recs, FaceData *__restrict__ fdata,
                                                             uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
                                                             uint2 *__restrict__ bins, uint32_t slab, int B,
-                                                            const ZeroFill zf, const float gx, const float gy)
+                                                            const ZeroFill zf, const float gx, const float gy,
+                                                            const uint32_t *__restrict__ stash_hdr = nullptr)
 {
     // workgroups past the faces zero-fill the caller's gradient accumulators (DIRT_FWD zero_grad_*): the
     // setup grid leaves most CUs idle (196 workgroups at config 3), so the fill costs the raster nothing
@@ -292,6 +305,9 @@ __global__ __launch_bounds__(NT) void setup_kernel(const float *__restrict__ ver
         zf.run((int64_t)blockIdx.y * (gridDim.x - zf.nfb) + (blockIdx.x - zf.nfb), (int64_t)(gridDim.x - zf.nfb) * gridDim.y);
         return;
     }
+    // the recompute backward's setup: nothing to do when the workspace already holds this geometry's records
+    // (stash hit, dirt_raster.hip stash_check_kernel)
+    if (stash_hdr != nullptr && stash_hit(stash_hdr)) return;
     __shared__ uint32_t hist[kMaxCoarse];
     __shared__ uint32_t base[kMaxCoarse];
     __shared__ BigQueue Q;
@@ -467,7 +483,8 @@ constexpr int kSetupSmallThreads = DIRT_SETUP_SMALL_THREADS;
 template <int AB = 0>
 void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int W, int V, int F, const Layout &L,
                   Rec *recs, FaceData *fdata, uint32_t *ccount, uint32_t *flag, uint2 *bins, hipStream_t stream,
-                  float *zero_a = nullptr, int64_t nzero_a = 0, float *zero_b = nullptr, int64_t nzero_b = 0)
+                  float *zero_a = nullptr, int64_t nzero_a = 0, float *zero_b = nullptr, int64_t nzero_b = 0,
+                  const uint32_t *stash_hdr = nullptr)
 {
     const bool small = (int64_t)B * ((F + kBinThreads - 1) / kBinThreads) < kSetupSmallGrid;
     const int nt = small ? kSetupSmallThreads : kBinThreads;
@@ -481,9 +498,9 @@ void launch_setup(const float *vertices, const int32_t *faces, int B, int H, int
     if (small)
         setup_kernel<AB, kSetupSmallThreads><<<grid, dim3(kSetupSmallThreads), 0, stream>>>(
             vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins, L.slab, B,
-            zf, gx, gy);
+            zf, gx, gy, stash_hdr);
     else
         setup_kernel<AB, kBinThreads><<<grid, dim3(kBinThreads), 0, stream>>>(
             vertices, faces, V, F, W, H, L.cshift, L.nctx, L.ncoarse, L.nrec, recs, fdata, ccount, flag, bins, L.slab, B,
-            zf, gx, gy);
+            zf, gx, gy, stash_hdr);
 }

@@ -10,9 +10,12 @@ and, like it, returns ONE tensor, pixels [B,H,W,C] -- so the reference's own wra
 Its gradient is registered the way a TensorFlow maintainer would register it for the single-output op
 (`@tf.RegisterGradient("Rasterise")`): from the op's inputs, its output and
 grad_pixels only, through `dirt_rasterise_bwd_recompute` (include/dirt_mi355x.h), which re-derives the
-g-buffer on the device as upstream DIRT's gradient did (csrc/rasterise_grad_common.h:5-24).  Nothing is kept
-between the forward and the backward except what autograd keeps for any op (inputs and output), and every
-buffer is allocated per call (TF's allocate_temp): no cached state, so the op is safe under graph capture.
+g-buffer on the device as upstream DIRT's gradient did (csrc/rasterise_grad_common.h:5-24) -- unless the op's
+workspace still holds it.  Round 5: the forward renders through `dirt_rasterise_fwd_stash`
+into a workspace cached per (device, stream, layout) -- the per-device resource a TF kernel pair would share -- and
+the gradient hands the same workspace to the recompute, which compares the geometry bitwise on the device and
+skips its recomputation when nothing changed (any other geometry in between costs one recomputation, never a
+wrong gradient).  The workspace is keyed by graph capture like the public op's scratch (a capture gets its own).
 
 The public `dirt_amd.rasterise` keeps the stateful backward (forward state kept for the gradient, no
 recomputation): it is the faster path; this module is the drop-in boundary the north star names.
@@ -33,34 +36,81 @@ class _RasteriseSingleOutput(torch.autograd.Function):
         B, V, F = vertices.shape[0], vertices.shape[1], faces.shape[1]
         dev = vertices.device
         lib = _lib.load()
-        saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, 0)
         pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
-        # temporaries of the forward only (TF: allocate_temp); the gradient recomputes what it needs
-        gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
-        saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
-        scratch = torch.empty((max(scratch_bytes, 1),), dtype=torch.uint8, device=dev)
         with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
-            cam = camera_pos.data_ptr() if camera_pos is not None else None
-            _lib.check(lib.dirt_rasterise_fwd(
-                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(), cam,
-                B, H, W, C, V, F, _lib.SHADER_GOURAUD, pixels.data_ptr(), gbuffer.data_ptr(),
-                saved.data_ptr(), saved_bytes, scratch.data_ptr(), scratch_bytes, 0, 0, None, None, stream))
-        # what TF hands a registered gradient: op.inputs and op.outputs
+            nbytes = _lib.recompute_workspace_size(B, H, W, C, V, F)
+            ws = _stash_workspaces.get(dev, stream, (B, H, W, C, V, F), nbytes)
+            # (camera_pos is read by the procedural programs only; Gouraud ignores it)
+            _lib.check(lib.dirt_rasterise_fwd_stash(
+                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
+                B, H, W, C, V, F, pixels.data_ptr(), ws.data_ptr(), nbytes, _lib.FWD_SCRATCH_CLEAN, stream))
+        # what TF hands a registered gradient: op.inputs and op.outputs (+ the op's workspace resource)
         ctx.save_for_backward(background, vertices, vertex_colors, faces, pixels)
         ctx.dims = (B, H, W, C, V, F)
+        ctx.workspace = ws
         return pixels
 
     @staticmethod
     def backward(ctx, grad_pixels):
         background, vertices, vertex_colors, faces, pixels = ctx.saved_tensors
-        return rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, ctx.dims) \
-            + (None,) * 5
+        return rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, ctx.dims,
+                                        workspace=ctx.workspace) + (None,) * 5
 
 
-def rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, dims=None):
+class _StashWorkspaces:
+    """Zero-filled recompute workspaces per (device, stream, layout[, capture id]), LRU of a few layouts.  Every
+    forward-stash and recompute leaves one clean (DIRT_BWD_SCRATCH_CLEAN); a capture gets workspaces of its own
+    (allocated in its graph's pool, zero-filled by a captured memset), as rasterise_ops._Workspace."""
+
+    def __init__(self, keep=4):
+        import collections
+        import threading
+        self.keep = keep
+        self._lock = threading.Lock()
+        self._d = collections.OrderedDict()
+        self._cap_id, self._cap = 0, {}
+
+    def get(self, dev, stream, layout, nbytes):
+        cid = _lib.capture_id(stream) if torch.cuda.is_current_stream_capturing() else 0
+        key = (dev, stream, layout)
+        with self._lock:
+            if cid:
+                if cid != self._cap_id:
+                    self._cap_id, self._cap = cid, {}
+                t = self._cap.get(key)
+            else:
+                t = self._d.get(key)
+                if t is not None:
+                    self._d.move_to_end(key)
+            if t is not None:
+                return t
+        t = torch.zeros((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+        with self._lock:
+            if cid:
+                if cid == self._cap_id:
+                    self._cap[key] = t
+            else:
+                self._d[key] = t
+                while len(self._d) > self.keep:
+                    self._d.popitem(last=False)
+        return t
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+            self._cap = {}
+
+
+_stash_workspaces = _StashWorkspaces()
+
+
+def rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, dims=None,
+                             workspace=None):
     """The registered gradient of the single-output op: (grad_background, grad_vertices, grad_vertex_colors)
-    from the op's inputs, its output `pixels` and `grad_pixels` (C ABI dirt_rasterise_bwd_recompute)."""
+    from the op's inputs, its output `pixels` and `grad_pixels` (C ABI dirt_rasterise_bwd_recompute).
+    `workspace`: the op's workspace (its forward's stash, DIRT_BWD_SCRATCH_CLEAN); None = a fresh one (the
+    recomputation always runs)."""
     if dims is None:
         B, H, W, C = pixels.shape
         dims = (B, H, W, C, vertices.shape[1], faces.shape[1])
@@ -69,7 +119,10 @@ def rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels,
     lib = _lib.load()
     grad_pixels = grad_pixels.to(dtype=torch.float32).contiguous()
     nbytes = _lib.recompute_workspace_size(B, H, W, C, V, F)
-    workspace = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    flags = _lib.BWD_SCRATCH_CLEAN
+    if workspace is None:
+        workspace = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+        flags = 0
     grad_vertices = torch.empty((B, V, 4), dtype=torch.float32, device=dev)
     grad_colors = torch.empty((B, V, C), dtype=torch.float32, device=dev)
     grad_background = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
@@ -78,7 +131,7 @@ def rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels,
         _lib.check(lib.dirt_rasterise_bwd_recompute(
             background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
             pixels.data_ptr(), grad_pixels.data_ptr(), B, H, W, C, V, F, grad_vertices.data_ptr(),
-            grad_colors.data_ptr(), grad_background.data_ptr(), workspace.data_ptr(), nbytes, 0, stream))
+            grad_colors.data_ptr(), grad_background.data_ptr(), workspace.data_ptr(), nbytes, flags, stream))
     return grad_background, grad_vertices, grad_colors
 
 

@@ -73,7 +73,8 @@ extern "C" {
  * 5: setup bins directly into fixed-capacity per-coarse-tile slabs, 3 profiled kernels; 6: bin counters on
  * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer; 8: + dirt_rasterise_bwd_recompute,
  * dirt_bwd_recompute_workspace_size; 9: + the fused lighting helpers dirt_vertex_normals_*,
- * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*; 10: + dirt_stream_capture_id) */
+ * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*; 10: + dirt_stream_capture_id;
+ * 11: + dirt_rasterise_fwd_stash, the recompute workspace grows by the gradient stash) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -174,7 +175,22 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
                                  void *workspace, size_t workspace_bytes, unsigned flags, void *stream);
 /* flags of dirt_rasterise_bwd_recompute: DIRT_BWD_ACCUMULATE, and */
 #define DIRT_BWD_SCRATCH_CLEAN 2u /* the workspace was zero-filled once and since used only by recompute
-                                     backwards of the same B, H, W, F: skip the bin-counter memset */
+                                     backwards and forward-stashes of the same B, H, W, V, F: skip the bin-counter
+                                     memset, and keep the gradient stash */
+/* Gradient stash (v11).  The workspace also records the geometry (vertices and faces, bitwise) whose setup records,
+ * g-buffer and coverage bits it holds.  dirt_rasterise_bwd_recompute first compares its vertices and faces with that
+ * record on the device: when they are identical it skips the recomputation (device-side: the setup and coverage
+ * launches exit at once) and runs the backward kernel on what the workspace holds -- the same gradients, since those
+ * intermediates are a deterministic function of the geometry and the frame size.  Otherwise it recomputes, and
+ * records the new geometry.  dirt_rasterise_fwd_stash is the single-output op's forward that fills the stash as it
+ * renders (pixels only as output; background / vertex colours do not enter the stash), so the gradient of that
+ * forward costs only the comparison: a TensorFlow kernel pair would share the workspace through a per-device
+ * resource keyed by the layout.  A different geometry in between (another render of the same layout) costs one
+ * recomputation, never a wrong gradient.  workspace: dirt_bwd_recompute_workspace_size() bytes; flags:
+ * DIRT_FWD_SCRATCH_CLEAN when the workspace is clean as DIRT_BWD_SCRATCH_CLEAN describes. */
+int dirt_rasterise_fwd_stash(const float *background, const float *vertices, const float *vertex_colors,
+                             const int32_t *faces, int B, int H, int W, int C, int V, int F, float *pixels,
+                             void *workspace, size_t workspace_bytes, unsigned flags, void *stream);
 
 /* Zero the bin counters of `scratch` for the next forward with the same B, H, W, F, bin_capacity
  * (an async memset of a few KB; lets a caller clear them on another stream, see DIRT_FWD_SCRATCH_CLEAN). */
