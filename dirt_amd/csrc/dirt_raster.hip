@@ -280,10 +280,29 @@ __global__ __launch_bounds__(256) void stash_check_kernel(const uint32_t *__rest
     if (__ballot(miss) != 0 && (threadIdx.x & 63) == 0) atomicOr(&hdr[kStashMiss + 16 * p], 1u);
 }
 
+// zero n bytes (a multiple of 4, 4-B aligned) with a kernel: the scratch / stash clears run inside HIP graphs that
+// the public op captures, and a kernel node is ordered like every other kernel of the graph
+__global__ __launch_bounds__(256) void zero_words_kernel(uint32_t *__restrict__ p, int64_t n)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) p[k] = 0u;
+}
+
 __global__ void stash_flip_kernel(uint32_t *p)
 {
     if (threadIdx.x == 0) p[0] ^= 1u;
 }
+
+// zero `bytes` (multiple of 4) at p on `stream` with zero_words_kernel
+int zero_async(void *p, size_t bytes, hipStream_t stream)
+{
+    const int64_t n = (int64_t)(bytes / 4);
+    if (n == 0) return DIRT_OK;
+    const unsigned blocks = (unsigned)std::min<int64_t>(1024, (n + 255) / 256);
+    zero_words_kernel<<<dim3(blocks), dim3(256), 0, stream>>>(static_cast<uint32_t *>(p), n);
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
+}
+
 
 // After a recomputation (this call's miss flag set), or unconditionally for a forward-stash (`force`): record the
 // geometry the workspace now holds.
@@ -371,7 +390,10 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
 
     // count sets and parity words: one memset, unless the caller vouches that the scratch is clean
     // (DIRT_FWD_SCRATCH_CLEAN: zeroed once and since used only by forwards of the same layout)
-    if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) HIP_TRY(hipMemsetAsync(ccount, 0, L.off_bins - L.off_count, stream));
+    if (!(flags & DIRT_FWD_SCRATCH_CLEAN)) {
+        rc = zero_async(ccount, L.off_bins - L.off_count, stream);
+        if (rc) return rc;
+    }
     // small scenes (Gouraud, F <= kFusedMaxF, at most kFusedMaxTiles tiles): the raster sets up the faces itself
     // (one launch, no bins)
     const bool fused = shader_id == DIRT_SHADER_GOURAUD && F > 0 && F <= kFusedMaxF &&
@@ -701,7 +723,10 @@ int dirt_rasterise_bwd_recompute(const float *background, const float *vertices,
     const bool acc = (flags & DIRT_BWD_ACCUMULATE) != 0;
     const bool clean = (flags & DIRT_BWD_SCRATCH_CLEAN) != 0;
     // (a workspace not vouched clean starts from scratch: bin counters and the stash header zeroed -- a miss)
-    if (!clean) HIP_TRY(hipMemsetAsync(hdr, 0, 256, stream));
+    if (!clean) {
+        rc = zero_async(hdr, 256, stream);
+        if (rc) return rc;
+    }
     // stash check: does the workspace already hold this geometry's records, g-buffer and coverage bits (left by
     // dirt_rasterise_fwd_stash or by the previous recomputation)?  The recomputation below then exits at once
     // (device-side; the setup's filler workgroups still zero the accumulators).
@@ -741,7 +766,10 @@ int dirt_rasterise_fwd_stash(const float *background, const float *vertices, con
     char *ws = static_cast<char *>(workspace);
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
     const bool clean = (flags & DIRT_FWD_SCRATCH_CLEAN) != 0;
-    if (!clean) HIP_TRY(hipMemsetAsync(ws + P.off_hdr, 0, 256, stream));
+    if (!clean) {
+        rc = zero_async(ws + P.off_hdr, 256, stream);
+        if (rc) return rc;
+    }
     rc = rasterise_fwd_impl(background, C, vertices, vertex_colors, faces, nullptr, B, H, W, C, V, F,
                             DIRT_SHADER_GOURAUD, pixels, reinterpret_cast<int32_t *>(ws + P.off_gbuf), ws,
                             L.saved_total, ws + P.off_scratch, L.scratch_total, 0, clean ? DIRT_FWD_SCRATCH_CLEAN : 0u,
@@ -1041,8 +1069,7 @@ int dirt_scratch_clear(int B, int H, int W, int F, int64_t bin_capacity, void *s
     if (!scratch || scratch_bytes < L.scratch_total)
         return fail(DIRT_EINVAL, "dirt_scratch_clear: scratch smaller than dirt_workspace_sizes()");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
-    HIP_TRY(hipMemsetAsync(static_cast<char *>(scratch) + L.off_count, 0, L.off_bins - L.off_count, stream));
-    return DIRT_OK;
+    return zero_async(static_cast<char *>(scratch) + L.off_count, L.off_bins - L.off_count, stream);
 }
 
 int dirt_stream_capture_id(void *stream_, unsigned long long *capture_id)
@@ -1086,7 +1113,9 @@ int dirt_vertex_normals_fwd(const float *vertices, int vertex_stride, const void
     const int64_t nv = (int64_t)B * V;
     if (nv == 0) return DIRT_OK;
     if (!vertices || !summed || !normals || (F > 0 && !faces)) return fail(DIRT_EINVAL, "vertex_normals: null pointer");
-    HIP_TRY(hipMemsetAsync(summed, 0, (size_t)nv * 3 * sizeof(float), stream));
+    int rc_z;
+    rc_z = zero_async(summed, (size_t)nv * 3 * sizeof(float), stream);  // (a kernel: graph-captured like the rest)
+    if (rc_z) return rc_z;
     if (F > 0 && B > 0) {
         const dim3 grid(light_blocks(F), (unsigned)B);
         if (faces_int64)
@@ -1113,7 +1142,8 @@ int dirt_vertex_normals_bwd(const float *vertices, int vertex_stride, const void
     if (nv == 0) return DIRT_OK;
     if (!vertices || !summed || !grad_normals || !grad_summed || !grad_vertices || (F > 0 && !faces))
         return fail(DIRT_EINVAL, "vertex_normals: null pointer");
-    HIP_TRY(hipMemsetAsync(grad_vertices, 0, (size_t)nv * grad_stride * sizeof(float), stream));
+    const int rc_z = zero_async(grad_vertices, (size_t)nv * grad_stride * sizeof(float), stream);
+    if (rc_z) return rc_z;
     if (F == 0) return DIRT_OK;
     vnormals_vertex_bwd_kernel<<<dim3(light_blocks(nv)), dim3(kLightThreads), 0, stream>>>(summed, grad_normals, nv,
                                                                                           grad_summed);

@@ -116,6 +116,12 @@ struct ScratchCache {
             }
         return nullptr;
     }
+    static bool debug()
+    {
+        static int v = -1;
+        if (v < 0) v = getenv("DIRT_DEBUG_SCRATCH") != nullptr;
+        return v != 0;
+    }
     at::Tensor get(const Key &k, size_t bytes, const at::Device &dev, hipStream_t stream)
     {
         const unsigned long long cid = capture_id(stream);
@@ -125,9 +131,13 @@ struct ScratchCache {
                 cap_id = cid;
                 cap.clear();
             }
-            if (at::Tensor *t = find(cid ? cap : lru, k, !cid)) return *t;
+            if (at::Tensor *t = find(cid ? cap : lru, k, !cid)) {
+                if (debug()) fprintf(stderr, "[dirt scratch] hit stream %p capture %llu ptr %p\n", (void *)stream, cid, t->data_ptr());
+                return *t;
+            }
         }
         at::Tensor t = at::empty({(int64_t)std::max<size_t>(bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
+        if (debug()) fprintf(stderr, "[dirt scratch] new stream %p capture %llu ptr %p\n", (void *)stream, cid, t.data_ptr());
         check(g_api.scratch_clear((int)std::get<2>(k), (int)std::get<3>(k), (int)std::get<4>(k), (int)std::get<5>(k),
                                   std::get<6>(k), t.data_ptr(), bytes, stream));
         std::lock_guard<std::mutex> g(mu);

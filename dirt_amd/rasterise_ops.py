@@ -19,6 +19,7 @@ There is no CPU path: the op requires a HIP device and raises if the native libr
 """
 import collections
 import os
+import sys
 import threading
 
 import numpy as np
@@ -62,6 +63,9 @@ class _on_device:
             self.ctx.__exit__(*a)
 
 
+_DEBUG_SCRATCH = os.environ.get("DIRT_DEBUG_SCRATCH") is not None
+
+
 class _Workspace:
     """Per-(device, stream, layout) cache of the forward-only scratch (tile bins, bin counters).
 
@@ -100,10 +104,14 @@ class _Workspace:
                 if t is not None:
                     self._d.move_to_end(key)
             if t is not None:
+                if _DEBUG_SCRATCH:
+                    print("[dirt scratch py] hit stream %x capture %d ptr %x" % (stream, cid, t.data_ptr()), file=sys.stderr)
                 return t
         # only the bin counters need zeroing (dirt_scratch_clear: a memset of the counter lines); the slabs
         # are written before they are read.  Under capture the memset is part of the graph.
         t = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+        if _DEBUG_SCRATCH:
+            print("[dirt scratch py] new stream %x capture %d ptr %x" % (stream, cid, t.data_ptr()), file=sys.stderr)
         B, H, W, F, cap = layout
         _lib.check(_lib.load().dirt_scratch_clear(B, H, W, F, cap, t.data_ptr(), nbytes, stream))
         with self._lock:

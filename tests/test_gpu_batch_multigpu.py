@@ -303,13 +303,21 @@ def test_two_graphs_same_layout_second_replayed_first(impl):
     scenes_ = [tuple(a[None] for a in scenes.random_triangles(F=2500, W=160, H=128, radius_px=10.0, seed=s))
                for s in (90, 91)]
     B, H, W, C = scenes_[0][0].shape
-    graphs, outs, refs = [], [], []
+    graphs, outs, refs, keep = [], [], [], []
     for bg, v, c, f in scenes_:
         t = [_gpu(a).requires_grad_(True) for a in (bg, v, c)]
         ft = _gpu(f)
         g = torch.randn(bg.shape, device="cuda")
-        px, _ = op(t[0], t[1], t[2], ft, H, W, C)
-        refs.append((px.detach().clone(), [x.clone() for x in torch.autograd.grad(px, t, g)]))
+        keep.append((t, ft, g))  # a graph's inputs must outlive it (the loop rebinds t, ft, g)
+        # (the eager reference on a side stream: an eager fwd + autograd backward of the op on the legacy default
+        # stream before a capture on another stream segfaulted in torch's capture_end on this stack --
+        # tools/debug/capture_repro2.py)
+        s_ = torch.cuda.Stream()
+        s_.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_):
+            px, _ = op(t[0], t[1], t[2], ft, H, W, C)
+            refs.append((px.detach().clone(), [x.clone() for x in torch.autograd.grad(px, t, g)]))
+        torch.cuda.synchronize()
         out = {}
 
         def step(t=t, ft=ft, g=g, out=out):
@@ -317,6 +325,12 @@ def test_two_graphs_same_layout_second_replayed_first(impl):
             out["px"] = px
             out["grads"] = torch.autograd.grad(px, t, g)
 
+        # warm-up on a side stream (lazy autograd / allocator initialisation must not happen inside a capture), then
+        # capture on torch.cuda.graph's class-wide default capture stream: both graphs share (device, stream, layout)
+        with torch.cuda.stream(s_):
+            step()
+        torch.cuda.current_stream().wait_stream(s_)
+        torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             step()
@@ -331,6 +345,53 @@ def test_two_graphs_same_layout_second_replayed_first(impl):
         for a, b in zip(outs[k]["grads"][1:], refs[k][1][1:]):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
     del graphs
+    rasterise_ops.workspace_cache_clear(force=True)
+
+
+def test_captured_scratch_clear_is_ordered_in_the_graph():
+    """A scratch created inside a capture is cleared by a node of that graph at every replay.  With the clear as a
+    hipMemsetAsync node the bin counters were not clean at the next replay on this stack (they grew by 61,440 per
+    replay, so every tile took the exact but slow all-records path, tools/debug/capture_repro4.py); the clear is a
+    kernel since round 5.  Replay a captured forward several times: the fullest slab stays at the eager count."""
+    import ctypes
+    from dirt_amd import _lib, rasterise_ops
+    rasterise_ops.workspace_cache_clear(force=True)
+    bg, v, c, f = (a[None] for a in scenes.random_triangles(F=2500, W=160, H=128, radius_px=10.0, seed=92))
+    B, H, W, C = bg.shape
+    F = f.shape[1]
+    t = [_gpu(a) for a in (bg, v, c, f)]
+
+    def fwd():
+        return rasterise_ops._RasteriseFunction.apply(t[0], t[1], t[2], t[3], None, H, W, C, 0, 0, False, False)
+
+    lib = _lib.load()
+    fn = lib.dirt_debug_bin_occupancy
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int] * 4 + [ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p] + \
+        [ctypes.POINTER(ctypes.c_uint32)] * 3
+
+    def max_count(scratch):
+        mx, ov, slab = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _lib.check(fn(B, H, W, F, 0, scratch.data_ptr(), scratch.numel(), torch.cuda.current_stream().cuda_stream,
+                      ctypes.byref(mx), ctypes.byref(ov), ctypes.byref(slab)))
+        return mx.value, ov.value
+
+    s_ = torch.cuda.Stream()
+    s_.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s_):
+        ref = fwd()[0].clone()
+    torch.cuda.synchronize()
+    eager = max_count(next(iter(rasterise_ops._workspace._d.values())))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = fwd()
+    scratch = next(iter(rasterise_ops._workspace._cap.values()))
+    for _ in range(4):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], ref)
+        assert max_count(scratch) == eager, (max_count(scratch), eager)
+    del graph
     rasterise_ops.workspace_cache_clear(force=True)
 
 
