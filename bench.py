@@ -37,6 +37,8 @@ CONFIGS = {
     "c3": (1, 1024, 1024, 3, 50000, 16.0),
     "c5": (8, 1024, 1024, 3, 20000, 16.0),  # 64 frames over 8 GPUs -> 8 per rank
     "c3_r64": (1, 1024, 1024, 3, 50000, 64.0),
+    # config 3 frames eight to a launch (profiling: the kernels' steady state, no single-round ramp or drain tail)
+    "c3x8": (8, 1024, 1024, 3, 50000, 16.0),
 }
 
 
@@ -631,6 +633,39 @@ def main():
             "value_eager_without": round(world * B * H * W * n_s / t_plain / 1e6, 1),
             "value_with_allreduce": round(world * B * H * W * n_s / t_ar / 1e6, 1),
             "ms_per_step_with_allreduce": round(t_ar * 1e3 / n_s, 4)}
+
+    def batched_leg():
+        """The same frames eight to a launch (config 3 x 8): the kernels at their steady state, without a single
+        frame's launch ramp and drain (profiles/r05/pmc_bound/README.md) -- the rate the batched configuration
+        C5 runs at.  Per-frame kernel times by HIP events and the backward's HBM fractions on them."""
+        cfg8 = CONFIGS["c3x8"]
+        B8 = cfg8[0]
+        _, (bg8, v8, c8, f8), g8, _ = make_inputs(cfg8, rank, device)
+        s8 = RasteriseSession(B8, H, W, C, V, F, device=device)
+
+        def step8():
+            s8.forward(bg8, v8, c8, f8)
+            s8.backward(g8)
+
+        for _ in range(3):
+            step8()
+        n8 = max(5, args.steps // 8)
+        g_8 = graph_of(step8, n8, cap_stream) if not args.no_graph else None
+        t8 = timed(g_8.replay if g_8 else lambda: [step8() for _ in range(n8)], 1, barrier, world, device, shared)
+        k8 = kernel_times(step8, max(2, args.profile_steps // 8))
+        per = {k: u / B8 for k, u in k8.items()}
+        out8 = {"what": "%d config-3 frames per launch (seeds %d..), per-frame kernel times by HIP events" % (B8, rank * B8),
+                "mpix_s": round(world * B8 * H * W * n8 / t8 / 1e6, 1),
+                "kernels_us_per_frame": {k: round(u, 2) for k, u in per.items()},
+                "grad_kernel_frac": round(kbytes["grad_kernel"] / (per["grad_kernel"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        if traffic is not None and dom == "grad_kernel":
+            out8["grad_traffic_frac"] = round(traffic / (per["grad_kernel"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        legs["batched_steady_state"] = out8
+        del g_8, s8
+
+    # ---- leg: eight frames per launch, the kernels' steady state (config 3 only)
+    if args.config == "c3" and args.rotate > 1:
+        leg("batched_steady_state", batched_leg)
 
     # ---- leg (N > 1): the shared-parameter gradient all-reduce of a data-parallel pose fit
     if world > 1 and not args.no_gather_leg:

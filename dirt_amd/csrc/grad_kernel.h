@@ -450,7 +450,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
         const int32_t g = s_gb[kme];
         const int key = g >= 0 ? g : -1;
         const int start = run_start(key, lr);
-        int slot = slot_insert_wave(T, key, key >= 0 && start == lr);
+        // (AB & 512, ablation: the slot table handed over instead of built -- slots from the key, no CAS inserts;
+        // timing only, wrong gradients)
+        int slot = (AB & 512) ? (key >= 0 && start == lr ? (key & 31) : -1) : slot_insert_wave(T, key, key >= 0 && start == lr);
         if (key >= 0 && start == lr && slot >= 0) atomicAdd(&s_tcnt[slot], 1);  // one run (one tail later)
         slot = __shfl(slot, (t & 48) + start, 64);
         s_slot[kme] = key >= 0 ? slot : -1;
@@ -458,8 +460,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     __syncthreads();
     PHASE_TS(2);
     PHASE_TS(3);
-    const int nslots = T.n;
+    const int nslots = (AB & 512) ? 32 : T.n;
     static_assert(kSlots <= 64, "one slot per lane of wave 0");
+    if ((AB & 512) && t < 32) T.list[t] = (int8_t)t;
     if (t < 64) {
         // wave 0: each slot's range of run-tail partials, in slot-list order (exclusive prefix)
         const int sl = t < nslots ? T.list[t] : 0;
@@ -483,7 +486,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
         EdgePart ep{};
         FaceData fd{};
         float riw0 = 0.f, riw1 = 0.f, riw2 = 0.f;
-        if (filler) {
+        if (filler && (AB & 512)) {
+            // (ablation: no record / FaceData round trip; made-up small edges and spread vertex ids)
+            sf = t;
+            for (int k = 0; k < 3; ++k) { ep.A[k] = 100 + k; ep.B[k] = -50 + k; fd.v[k] = (int)(((unsigned)blockIdx.x * 96u + 3u * t + k) % (unsigned)max(V, 1)); fd.q[k] = 1.0f; }
+            ep.D = 5000; ep.i0 = 0; ep.i1 = 1000; ep.j0 = 0; ep.j1 = 1000; ep.X0 = 0; ep.Y0 = 0;
+        } else if (filler) {
             sf = T.list[t];
             const int32_t ri = T.key[sf] & kGbufIndexMask;
             ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
