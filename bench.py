@@ -671,6 +671,13 @@ def main():
     if world > 1 and not args.no_gather_leg:
         leg("shared_allreduce", allreduce_leg)
 
+    # R5 deviation counters over every forward the headline session ran: faces culled by the R5
+    # vertex cap, clipped faces moved by the R5 sub-vertex clamp (0 expected on these scenes)
+    try:
+        clip_stats = sess.clip_stats()
+    except Exception as e:  # noqa: BLE001 -- informative field only
+        clip_stats = {"error": str(e)[:200]}
+
     cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref = cpu_baseline(host, grad_host, budget_s=args.cpu_budget)
@@ -694,6 +701,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_vs_oracle": par,
+            "r5_clip_stats": clip_stats,
             "kernels_us": {k: round(u, 2) for k, u in kern_us.items()},
             "legs": legs,
         }
