@@ -27,10 +27,11 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
-FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes
+FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes (forced; automatic since ABI 12)
+FWD_DEEP_CULL_OFF = 8  # dirt_rasterise_fwd: never the occluder culling
 BWD_ACCUMULATE = 1     # dirt_rasterise_bwd / dirt_rasterise_bwd_recompute flags
 BWD_SCRATCH_CLEAN = 2  # dirt_rasterise_bwd_recompute: the workspace's bin counters are clean
 
@@ -155,6 +156,19 @@ def stash_state(B, H, W, C, V, F, workspace, workspace_bytes, stream):
     miss, magic = ctypes.c_uint32(0), ctypes.c_uint32(0)
     check(fn(B, H, W, C, V, F, workspace, workspace_bytes, stream, ctypes.byref(miss), ctypes.byref(magic)))
     return {"last_missed": miss.value, "magic": magic.value}
+
+
+def deep_cull_state():
+    """Debug: the automatic deep-scene culling rule of the current device -- {"gen": forwards issued with it,
+    "last_deep": generation of the last forward reported deep (0 = none), "next_deep": whether the next forward
+    takes the occluder-culling raster}.  Reflects the launches the device has executed so far (no sync)."""
+    lib = load()
+    fn = lib.dirt_debug_deep_cull_state
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int)]
+    gen, last, nxt = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+    check(fn(ctypes.byref(gen), ctypes.byref(last), ctypes.byref(nxt)))
+    return {"gen": gen.value, "last_deep": last.value, "next_deep": bool(nxt.value)}
 
 
 NUM_KERNELS = 3

@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(256) void stash_update_kernel(const uint32_t *__res
 
 extern "C" {
 
-int dirt_abi_version(void) { return 11; }
+int dirt_abi_version(void) { return 12; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -346,6 +347,56 @@ int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_c
 }
 
 }  // extern "C"
+
+// Automatic deep-scene culling: the Gouraud raster counts its long per-wave entry lists
+// (raster_kernel deep_host), and the next launch on the same scratch reports whether that count made the launch deep
+// by writing its generation into a host-mapped word per device.  A forward takes the occluder-culling
+// instantiation (OCC) when a launch within the last kDeepRecent generations was deep: a deep scene switches after
+// one launch (plus the queue's lag), a scene turning shallow switches back after kDeepRecent.  Both instantiations are
+// exact, so the choice changes time only.  DIRT_FWD_DEEP_CULL forces OCC, DIRT_FWD_DEEP_CULL_OFF the plain raster;
+// DIRT_DEEP_CULL_AUTO=0 disables the rule.
+// A stream under graph capture uses the word only once it exists (no allocation during a capture).
+constexpr uint32_t kDeepRecent = 8;
+struct DeepAuto {
+    uint32_t *host = nullptr;  // host-mapped word: generation of the last launch reported deep (0 = none)
+    uint32_t *dev = nullptr;   // its device address
+    uint32_t gen = 0;          // launches issued with the rule on
+};
+static std::mutex g_deep_mu;
+static DeepAuto g_deep[64];
+
+static bool deep_auto_enabled()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("DIRT_DEEP_CULL_AUTO");
+        v = (e && *e) ? (atoi(e) != 0) : 1;
+    }
+    return v != 0;
+}
+
+// the device's state with its word allocated (nullptr: rule off or no word yet and the stream is capturing)
+static DeepAuto *deep_auto_state(hipStream_t stream)
+{
+    if (!deep_auto_enabled()) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    DeepAuto &d = g_deep[dev];
+    std::lock_guard<std::mutex> lk(g_deep_mu);
+    if (d.host) return &d;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    void *h = nullptr, *dp = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return nullptr;
+    }
+    static_cast<volatile uint32_t *>(h)[0] = 0u;
+    d.dev = static_cast<uint32_t *>(dp);
+    d.host = static_cast<uint32_t *>(h);
+    return &d;
+}
 
 // the forward of every op; tcb = channels of `background` (== C except for hill's terrain lookup)
 static int rasterise_fwd_impl(const float *background, int tcb, const float *vertices, const float *vertex_colors,
@@ -398,8 +449,26 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     // (one launch, no bins)
     const bool fused = shader_id == DIRT_SHADER_GOURAUD && F > 0 && F <= kFusedMaxF &&
                        (int64_t)B * L.ntiles <= kFusedMaxTiles;
-    // occluder culling of long per-wave entry lists (deep scenes), opt-in (raster_kernel.h, OCC)
-    const bool deep = (flags & DIRT_FWD_DEEP_CULL) != 0 && shader_id == DIRT_SHADER_GOURAUD && !nopix;
+    // occluder culling of long per-wave entry lists (deep scenes, raster_kernel.h OCC): forced by DIRT_FWD_DEEP_CULL,
+    // else automatic (DeepAuto) for the binned Gouraud forward
+    bool deep = (flags & DIRT_FWD_DEEP_CULL) != 0 && shader_id == DIRT_SHADER_GOURAUD && !nopix;
+    uint32_t *deep_host = nullptr, deep_gen = 0;
+    if (shader_id == DIRT_SHADER_GOURAUD && !nopix && !fused && !want_gb && F > 0 && !(flags & DIRT_FWD_DEEP_CULL_OFF)) {
+        if (DeepAuto *da = deep_auto_state(stream)) {
+            // (a launch captured into a graph does not count as a generation: it does not execute now, and a long
+            // capture would otherwise age the device's last report past kDeepRecent; its replays repeat the
+            // generation of the capture)
+            hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+            const bool capturing = hipStreamIsCapturing(stream, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
+            std::lock_guard<std::mutex> lk(g_deep_mu);
+            if (!capturing) ++da->gen;
+            if (da->gen == 0) da->gen = 1;  // (0 means "never deep")
+            deep_gen = da->gen;
+            const uint32_t last = static_cast<volatile uint32_t *>(da->host)[0];
+            deep = deep || (last != 0u && deep_gen - last <= kDeepRecent);
+            deep_host = da->dev;
+        }
+    }
     if (F > 0 && !fused) {
         ProfScope ps(K_SETUP, stream);
         launch_setup<0>(vertices, faces, B, H, W, V, F, L, recs, fdata, ccount, flag, bins, stream, zero_grad_vertices,
@@ -444,7 +513,8 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
             L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
             zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
-            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb);               \
+            zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, GbufOut{},      \
+            nullptr, nullptr, deep_host, deep_gen);                                                              \
     else if (fused && want_gb)                                                                                   \
         raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, true, true><<<grid, dim3(256), 0, stream>>>(                   \
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
@@ -472,7 +542,8 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
                                                       zero_grad_vertices ? (int64_t)B * V * 4 : 0,                 \
                                                       zero_grad_vertex_colors,                                     \
                                                       zero_grad_vertex_colors ? (int64_t)B * V * C : 0,            \
-                                                      vertices, camera_pos, shader_id, tcb)
+                                                      vertices, camera_pos, shader_id, tcb, GbufOut{}, nullptr,    \
+                                                      nullptr, deep_host, deep_gen)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else if (C == 7) LAUNCH_RASTER(7);
@@ -840,6 +911,23 @@ int dirt_debug_clip_stats(int B, int H, int W, int F, int64_t bin_capacity, void
     HIP_TRY(hipStreamSynchronize(stream));
     if (cap_culled) *cap_culled = h[0];
     if (clamped) *clamped = h[1];
+    return DIRT_OK;
+}
+
+// Debug: the automatic deep-cull rule of the current device (DeepAuto): launches issued with it, the generation of
+// the last launch reported deep (0 = none), and whether the next forward would take the occluder instantiation.
+// Not part of include/dirt_mi355x.h.
+int dirt_debug_deep_cull_state(uint32_t *gen, uint32_t *last_deep, int *next_deep)
+{
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(DIRT_EINVAL, "dirt_debug_deep_cull_state: device index");
+    std::lock_guard<std::mutex> lk(g_deep_mu);
+    const DeepAuto &d = g_deep[dev];
+    const uint32_t last = d.host ? static_cast<volatile uint32_t *>(d.host)[0] : 0u;
+    if (gen) *gen = d.gen;
+    if (last_deep) *last_deep = last;
+    if (next_deep) *next_deep = (last != 0u && d.gen + 1u - last <= kDeepRecent) ? 1 : 0;
     return DIRT_OK;
 }
 

@@ -358,10 +358,12 @@ def workspace_cache_size():
 
 # DIRT_CHECK_FACES=1: every call range-checks its face indices (one kernel + a host sync; off by default)
 _CHECK_FACES_DEFAULT = os.environ.get("DIRT_CHECK_FACES", "") not in ("", "0")
-# DIRT_DEEP_CULL=1: Gouraud forwards cull occluded triangles of long per-tile lists (DIRT_FWD_DEEP_CULL): for deep
-# scenes of large overlapping triangles; identical results, scenes of small triangles run slightly faster without
-_FWD_FLAGS = _lib.FWD_SCRATCH_CLEAN | (_lib.FWD_DEEP_CULL if os.environ.get("DIRT_DEEP_CULL", "") not in ("", "0")
-                                       else 0)
+# Gouraud forwards take the occluder culling of long per-tile lists by the library's automatic rule (ABI 12,
+# include/dirt_mi355x.h DIRT_FWD_DEEP_CULL); DIRT_DEEP_CULL=1 forces it, DIRT_DEEP_CULL=0 turns it off (identical
+# results either way)
+_DEEP_ENV = os.environ.get("DIRT_DEEP_CULL", "")
+_FWD_FLAGS = _lib.FWD_SCRATCH_CLEAN | (_lib.FWD_DEEP_CULL if _DEEP_ENV not in ("", "0") else
+                                       _lib.FWD_DEEP_CULL_OFF if _DEEP_ENV == "0" else 0)
 
 
 def _rasterise_batched(background, vertices, vertex_colors, faces, camera_pos, height, width, channels, shader_id,

@@ -24,10 +24,13 @@ from . import _lib
 
 
 class RasteriseSession:
-    def __init__(self, B, H, W, C, V, F, device=None, bin_capacity=0, shader_id=_lib.SHADER_GOURAUD, deep_cull=False):
-        """deep_cull: occluder culling for deep scenes (DIRT_FWD_DEEP_CULL: large overlapping triangles)."""
+    def __init__(self, B, H, W, C, V, F, device=None, bin_capacity=0, shader_id=_lib.SHADER_GOURAUD, deep_cull=None):
+        """deep_cull: occluder culling for deep scenes of large overlapping triangles -- None: the library's automatic
+        rule (the culling raster while one of the device's last 8 forwards was deep), True: always
+        (DIRT_FWD_DEEP_CULL), False: never (DIRT_FWD_DEEP_CULL_OFF).  The results are identical in every case."""
         self.dims = (B, H, W, C, V, F)
-        self.fwd_flags = _lib.FWD_SCRATCH_CLEAN | (_lib.FWD_DEEP_CULL if deep_cull else 0)
+        self.fwd_flags = _lib.FWD_SCRATCH_CLEAN | {None: 0, True: _lib.FWD_DEEP_CULL, False: _lib.FWD_DEEP_CULL_OFF}[
+            None if deep_cull is None else bool(deep_cull)]
         self.shader_id = shader_id
         dev = torch.device(device) if device is not None else torch.device("cuda")
         if dev.type == "cuda" and dev.index is None:  # "cuda" means the current device: compare as cuda:N

@@ -74,7 +74,8 @@ extern "C" {
  * separate 256-B lines of the scratch; 7: + dirt_rasterise_fwd_gbuffer; 8: + dirt_rasterise_bwd_recompute,
  * dirt_bwd_recompute_workspace_size; 9: + the fused lighting helpers dirt_vertex_normals_*,
  * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*; 10: + dirt_stream_capture_id;
- * 11: + dirt_rasterise_fwd_stash, the recompute workspace grows by the gradient stash) */
+ * 11: + dirt_rasterise_fwd_stash, the recompute workspace grows by the gradient stash; 12: the Gouraud forward
+ * picks the occluder culling by itself (DIRT_FWD_DEEP_CULL forces it, + DIRT_FWD_DEEP_CULL_OFF)) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -130,7 +131,12 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
 #define DIRT_FWD_DEEP_CULL 2u     /* Gouraud: occluder culling of long per-tile triangle lists before they are
                                      rasterised -- for deep scenes (large overlapping triangles: depth complexity
                                      ~45 at r = 64 px, raster -15 %); results are identical either way, and
-                                     scenes of small triangles run slightly faster without it */
+                                     scenes of small triangles run slightly faster without it.  Since ABI 12 the
+                                     binned Gouraud forward chooses it by itself: each launch counts its long
+                                     per-wave lists, and a device takes the culling raster while one of its last
+                                     8 forwards was deep (env DIRT_DEEP_CULL_AUTO=0 turns the rule off); this
+                                     flag forces it */
+#define DIRT_FWD_DEEP_CULL_OFF 8u /* Gouraud: never the occluder culling (the plain raster, as before ABI 12) */
 /* zero_grad_vertices [B,V,4] / zero_grad_vertex_colors [B,V,C] (each may be NULL): accumulators the
  * forward zero-fills in passing (filler workgroups of its setup launch, idle CUs), for a later dirt_rasterise_bwd with
  * DIRT_BWD_ACCUMULATE -- a fixed-shape training loop then pays no separate clearing launch.

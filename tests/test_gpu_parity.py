@@ -417,7 +417,7 @@ def test_deep_cull_flag_bit_exact(scene):
     bg, v, c, f = (a[None] for a in sc)
     g = np.random.default_rng(3).standard_normal(bg.shape).astype(np.float32)
     outs = []
-    for deep in (False, True):
+    for deep in (False, True, None):  # plain, forced, the automatic rule (ABI 12)
         sess = RasteriseSession(*bg.shape, v.shape[1], f.shape[1], device="cuda", deep_cull=deep)
         sess.forward(*(_gpu(a) for a in (bg, v, c, f)))
         gbg, gv, gc = (t.cpu().numpy() for t in sess.backward(_gpu(g)))
@@ -430,6 +430,65 @@ def test_deep_cull_flag_bit_exact(scene):
         np.testing.assert_array_equal(gbg, rgbg)
         assert_close_grad(gc, rgc, "grad_vertex_colors")
         assert_close_grad(gv, rgv, "grad_vertices")
+
+
+def test_deep_cull_automatic_rule():
+    """ABI 12: the binned Gouraud forward counts its long per-wave lists and a device takes the occluder-culling
+    raster while one of its last 8 forwards was deep.  A deep scene (r = 64 px triangles, depth complexity in the
+    hundreds) turns the rule on after one forward; config 3's small triangles never mark a launch deep, and after
+    8 of them the rule is off again.  Output identical to the oracle under the automatic choice."""
+    import torch
+    from dirt_amd import _lib
+    from dirt_amd.session import RasteriseSession
+    deep = scenes.random_triangles(F=6000, W=256, H=256, radius_px=64.0, seed=5)
+    shallow = scenes.random_triangles(F=50000, W=1024, H=1024, seed=0)
+    outs = {}
+    for name, sc in (("deep", deep), ("shallow", shallow)):
+        bg, v, c, f = (a[None] for a in sc)
+        sess = RasteriseSession(*bg.shape, v.shape[1], f.shape[1], device="cuda")
+        args = [_gpu(a) for a in (bg, v, c, f)]
+        before = _lib.deep_cull_state()
+        for _ in range(10):
+            sess.forward(*args)
+            torch.cuda.synchronize()
+        outs[name] = (before, _lib.deep_cull_state(), sess.pixels.cpu().numpy(), sess.gbuffer.cpu().numpy(),
+                      (bg, v, c, f))
+    b0, s0 = outs["deep"][:2]
+    assert s0["gen"] >= b0["gen"] + 10
+    assert s0["last_deep"] > b0["gen"], "the deep scene's forwards were not reported deep"
+    assert s0["next_deep"]
+    # forwards captured into a graph do not age the rule (they execute only at replay): a capture of more than
+    # kDeepRecent (8) forwards keeps the choice made before it for every captured step
+    bg, v, c, f = outs["deep"][4]
+    sess = RasteriseSession(*bg.shape, v.shape[1], f.shape[1], device="cuda")
+    args = [_gpu(a) for a in (bg, v, c, f)]
+    for _ in range(3):  # (a launch is reported by the next one on the same scratch)
+        sess.forward(*args)
+        torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        st0 = _lib.deep_cull_state()
+        with torch.cuda.graph(graph, stream=side):
+            for _ in range(12):
+                sess.forward(*args)
+        st1 = _lib.deep_cull_state()
+    assert st0["next_deep"]
+    assert st1["gen"] == st0["gen"] and st1["next_deep"]
+    graph.replay()
+    torch.cuda.synchronize()
+    px, gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+    np.testing.assert_array_equal(sess.pixels.cpu().numpy(), px)
+    del graph
+    b1, s1 = outs["shallow"][:2]
+    assert s1["last_deep"] == b1["last_deep"], "a config-3 forward was reported deep"
+    assert not s1["next_deep"]
+    for name in ("deep", "shallow"):
+        pix, gbuf, (bg, v, c, f) = outs[name][2:]
+        px, gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+        np.testing.assert_array_equal(gbuf, gb)
+        np.testing.assert_array_equal(pix, px)
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUZZ_FIRST", "0")),

@@ -157,7 +157,7 @@ def run(name, frames, steps=100):
     V, F = v.shape[1], f.shape[1]
     g = torch.randn((B, H, W, C), device=dev)
     cap = BIN_CAPACITY.get(name, 0)
-    sess = RasteriseSession(B, H, W, C, V, F, device=dev, bin_capacity=cap, deep_cull=name.endswith("deep_cull"))
+    sess = RasteriseSession(B, H, W, C, V, F, device=dev, bin_capacity=cap, deep_cull=True if name.endswith("deep_cull") else None)
 
     def step():
         sess.forward(bg, v, c, f)
