@@ -28,9 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
 # measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc passes of this bench at c3;
 # produced by tools/gpu_traffic.sh + tools/pmc_traffic.py, committed with the round's profiles)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04", "traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05", "traffic.json")
 if not os.path.exists(TRAFFIC_JSON):
-    TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "traffic.json")
+    TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04", "traffic.json")
 
 CONFIGS = {
     # name: (B per rank, H, W, C, F, radius_px)
