@@ -663,6 +663,33 @@ def main():
         legs["batched_steady_state"] = out8
         del g_8, s8
 
+    def deep_leg():
+        """The r = 64 px stress distribution (config 3's frame with large triangles, depth complexity ~45): the
+        default forward, which picks the occluder-culling raster by itself (ABI 12), against the plain
+        raster forced (DIRT_FWD_DEEP_CULL_OFF).  Graph-replayed fwd+bwd steps and the raster's event time."""
+        cfgd = CONFIGS["c3_r64"]
+        _, (bgd, vd, cd, fd), gd, _ = make_inputs(cfgd, rank, device)
+        out = {"what": "config-3 frame of r = 64 px triangles: automatic deep culling vs the plain raster"}
+        for name, dc in (("default", None), ("plain", False)):
+            sd = RasteriseSession(B, H, W, C, V, F, device=device, deep_cull=dc)
+
+            def stepd():
+                sd.forward(bgd, vd, cd, fd)
+                sd.backward(gd)
+
+            for _ in range(4):
+                stepd()
+            torch.cuda.synchronize()
+            nd = max(10, args.steps // 10)
+            g_d = graph_of(stepd, nd, cap_stream) if not args.no_graph else None
+            td = timed(g_d.replay if g_d else lambda: [stepd() for _ in range(nd)], 1, barrier, world, device, shared)
+            kd = kernel_times(stepd, max(2, args.profile_steps // 4))
+            out[name] = {"mpix_s": round(world * B * H * W * nd / td / 1e6, 1),
+                         "kernels_us": {k: round(u, 2) for k, u in kd.items()}}
+            del g_d, sd
+        out["rule_state"] = _lib.deep_cull_state()
+        legs["deep_scene"] = out
+
     # ---- leg: eight frames per launch, the kernels' steady state (config 3 only)
     if args.config == "c3" and args.rotate > 1:
         leg("batched_steady_state", batched_leg)
@@ -670,6 +697,11 @@ def main():
     # ---- leg (N > 1): the shared-parameter gradient all-reduce of a data-parallel pose fit
     if world > 1 and not args.no_gather_leg:
         leg("shared_allreduce", allreduce_leg)
+
+    # ---- leg: a deep scene under the default forward (config 3's shape, r = 64 px; last: it leaves the device's
+    # automatic deep-cull rule on for a few forwards)
+    if args.config == "c3" and args.rotate > 1:
+        leg("deep_scene", deep_leg)
 
     # R5 deviation counters over every forward the headline session ran: faces culled by the R5
     # vertex cap, clipped faces moved by the R5 sub-vertex clamp (0 expected on these scenes)
