@@ -33,6 +33,20 @@ def test_library_exports_every_declared_symbol():
     assert set(declared_functions()) <= set(_lib.SIGNATURES)
 
 
+def test_header_flags_match_the_binding():
+    """The flag values the header #defines are the ones dirt_amd._lib passes (ABI 12 adds DIRT_FWD_DEEP_CULL_OFF),
+    and the forward's flags are distinct bits."""
+    text = open(HEADER).read()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+(DIRT_(?:FWD|BWD)_\w+)\s+(\d+)u", text)}
+    assert defs["DIRT_FWD_SCRATCH_CLEAN"] == _lib.FWD_SCRATCH_CLEAN
+    assert defs["DIRT_FWD_DEEP_CULL"] == _lib.FWD_DEEP_CULL
+    assert defs["DIRT_FWD_DEEP_CULL_OFF"] == _lib.FWD_DEEP_CULL_OFF
+    assert defs["DIRT_BWD_ACCUMULATE"] == _lib.BWD_ACCUMULATE
+    assert defs["DIRT_BWD_SCRATCH_CLEAN"] == _lib.BWD_SCRATCH_CLEAN
+    fwd = [v for k, v in defs.items() if k.startswith("DIRT_FWD_")]
+    assert all(v & (v - 1) == 0 for v in fwd) and len(set(fwd)) == len(fwd)
+
+
 def test_abi_version_and_workspace_sizes():
     lib = _lib.load()
     assert lib.dirt_abi_version() == _lib.ABI_VERSION == 12
