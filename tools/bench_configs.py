@@ -33,6 +33,9 @@ CONFIGS = {
     "c3x8_random50k_1024x1024x3_batch8": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, seed=b)
                                                   for b in range(8)],
     "c4_deferred20k_512x512x7": lambda: [scenes.deferred_mesh_scene()],
+    # a quarter-size config-3 frame (one round of backward workgroups): the small-frame shape of the deferred renders
+    "c3q_random20k_512x512x3": lambda: [scenes.random_triangles(F=20000, W=512, H=512, seed=0)],
+    "c3q_mesh20k_512x512x3": lambda: [tuple(a[..., :3] if k in (0, 2) else a for k, a in enumerate(scenes.deferred_mesh_scene()))],
     "c5_batch8x20k_1024x1024x3_per_gpu": lambda: [scenes.random_triangles(F=20000, W=1024, H=1024, seed=b)
                                                   for b in range(8)],
     "c3_stress_r64_1024x1024x3": lambda: [scenes.random_triangles(F=50000, W=1024, H=1024, radius_px=64.0, seed=0)],
