@@ -432,6 +432,27 @@ def test_deep_cull_flag_bit_exact(scene):
         assert_close_grad(gv, rgv, "grad_vertices")
 
 
+def test_deep_cull_automatic_rule_through_the_public_op():
+    """The public op (dirt_amd.rasterise_batch + autograd, the C++ extension's path) under the automatic deep-cull
+    rule: a batch of two deep frames rendered repeatedly -- the later calls take the occluder-culling raster -- with
+    pixels bit-exact and gradients within tolerance of the oracle on every call."""
+    import dirt_amd
+    frames = [scenes.random_triangles(F=3000, W=160, H=128, radius_px=48.0, seed=40 + k) for k in range(2)]
+    bg, v, c, f = (np.stack([fr[k] for fr in frames]) for k in range(4))
+    g = np.random.default_rng(7).standard_normal(bg.shape).astype(np.float32)
+    px, gb, _ = oracle.rasterise_fwd(bg, v, c, f)
+    rgv, rgc, rgbg = oracle.rasterise_bwd(v, c, f, px, g, gb)
+    for _ in range(4):
+        bt, vt, ct = (_gpu(a).requires_grad_(True) for a in (bg, v, c))
+        out = dirt_amd.rasterise_batch(bt, vt, ct, _gpu(f), height=128, width=160, channels=3)
+        gbg, gv, gc = (t.cpu().numpy() for t in torch.autograd.grad(out, [bt, vt, ct], _gpu(g)))
+        np.testing.assert_array_equal(out.detach().cpu().numpy(), px)
+        np.testing.assert_array_equal(gbg, rgbg)
+        assert_close_grad(gc, rgc, "grad_vertex_colors")
+        assert_close_grad(gv, rgv, "grad_vertices")
+        torch.cuda.synchronize()
+
+
 def test_deep_cull_automatic_rule():
     """ABI 12: the binned Gouraud forward counts its long per-wave lists and a device takes the occluder-culling
     raster while one of its last 8 forwards was deep.  A deep scene (r = 64 px triangles, depth complexity in the
