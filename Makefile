@@ -30,7 +30,7 @@ ORACLE_CFLAGS = -O3 -std=c99 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wa
 LIB = dirt_amd/libdirt_mi355x.so
 ORACLE = oracle/libdirt_oracle.so
 HIP_SRC = dirt_amd/csrc/dirt_raster.hip
-HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/lighting_kernels.h dirt_amd/csrc/setup_kernel.h dirt_amd/csrc/raster_kernel.h dirt_amd/csrc/grad_kernel.h dirt_amd/csrc/grad_persist.h dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h Makefile
+HIP_DEPS = $(HIP_SRC) dirt_amd/csrc/lighting_kernels.h dirt_amd/csrc/setup_kernel.h dirt_amd/csrc/raster_kernel.h dirt_amd/csrc/grad_kernel.h dirt_amd/csrc/raster_rules.h dirt_amd/csrc/oceanic.h dirt_amd/csrc/hill.h include/dirt_mi355x.h Makefile
 
 # the public op's C++ autograd function (PyTorch extension over the C ABI; dirt_amd/csrc/torch_op.cpp)
 PY ?= python3

@@ -28,9 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
 # measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc passes of this bench at c3;
 # produced by tools/gpu_traffic.sh + tools/pmc_traffic.py, committed with the round's profiles)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05", "traffic.json")
-if not os.path.exists(TRAFFIC_JSON):
-    TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04", "traffic.json")
+# (the newest round's file; it names the tree and the box it was measured on, `measured_on`)
+TRAFFIC_JSON = next((p for p in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r06", "r05", "r04"))
+                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r06", "traffic.json"))
 
 CONFIGS = {
     # name: (B per rank, H, W, C, F, radius_px)
@@ -43,15 +43,19 @@ CONFIGS = {
 
 
 def alg_bytes(B, H, W, C, V, F):
-    """Algorithmic HBM bytes (tensor I/O of the op) per kernel and per op."""
-    hwc, hw = 4 * C * H * W, 4 * H * W
-    k = {
-        "raster_kernel": B * (2 * hwc + hw + 4 * C * V + 12 * F),
-        "grad_kernel": B * (3 * hwc + hw + 16 * V + 12 * F + 16 * V + 4 * C * V),
-        "setup_kernel": B * (12 * F + 16 * V),
-    }
+    """Algorithmic HBM bytes, SURVEY 8(d): the tensor I/O of the op's C ABI, intermediates (records, bins, the
+    g-buffer) excluded.  fwd = 16V + 12F + 4CV + 4CHW (background) + 4CHW (pixels); bwd = 16V + 12F + 4CV (inputs)
+    + 4CHW (pixels) + 4CHW (grad_pixels) + 16V + 4CV (gradient outputs) + 4CHW (grad_background) -- config 3:
+    29.96 + 46.75 MB.  Per kernel: the backward is the one grad launch (all of bwd); the forward's split is setup =
+    vertices + faces, raster = colours + background + pixels."""
+    hwc = 4 * C * H * W
     fwd = B * (16 * V + 12 * F + 4 * C * V + 2 * hwc)
     bwd = B * (16 * V + 12 * F + 4 * C * V + 2 * hwc + 16 * V + 4 * C * V + hwc)
+    k = {
+        "setup_kernel": B * (16 * V + 12 * F),
+        "raster_kernel": B * (4 * C * V + 2 * hwc),
+        "grad_kernel": bwd,
+    }
     return k, fwd, bwd
 
 
@@ -322,18 +326,30 @@ def main():
         except Exception as e:  # noqa: BLE001 -- informative field only
             print("graph pass timing failed: %s" % e, file=sys.stderr)
             torch.cuda.synchronize()
-    dom = max((k for k in kern_us if k in kbytes), key=lambda k: kern_us[k])
-    achieved = kbytes[dom] / (kern_us[dom] * 1e-6) / 1e9
-    traffic = None
+    # The roofline kernel is the backward scatter (grad_kernel), the kernel the north star states its bandwidth
+    # target on and the longest launch of the step by rocprofv3 (profiles/r06/).  achieved = SURVEY 8(d)'s backward
+    # bytes (46.75 MB at c3) / the kernel's average duration: HIP events on the launch stream around one replay of
+    # a graph of 50 backward launches (no launch gap; rocprofv3 --kernel-trace reports the same duration), else the
+    # eager event pairs (which include each launch's dependent-launch gap, reported beside as avg_us_events).
+    dom = "grad_kernel"
+    dom_events = max((k for k in kern_us if k in kbytes), key=lambda k: kern_us[k])
+    dur_us = pass_us["bwd_grad"] if pass_us else kern_us[dom]
+    achieved = kbytes[dom] / (dur_us * 1e-6) / 1e9
+    traffic = measured_on = None
     if args.config == "c3" and os.path.exists(TRAFFIC_JSON):
-        tk = json.load(open(TRAFFIC_JSON)).get("kernels", {})
-        hit = [v for k, v in tk.items() if k.split("<")[0] == dom]
+        tj = json.load(open(TRAFFIC_JSON))
+        hit = [v for k, v in tj.get("kernels", {}).items() if k.split("<")[0] == dom]
         if hit:
             traffic = hit[0]["traffic_bytes"]
+            measured_on = tj.get("measured_on")
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic is not None else None,
-                "alg_bytes_per_launch": kbytes[dom], "avg_us": round(kern_us[dom], 2),
+                "traffic_measured_on": measured_on,
+                "alg_bytes_per_launch": kbytes[dom], "alg_bytes_definition": "SURVEY 8(d) bwd",
+                "avg_us": round(dur_us, 2),
+                "avg_us_source": "graph of 50 launches, HIP events" if pass_us else "eager HIP event pairs",
+                "avg_us_events": round(kern_us[dom], 2), "dominant_kernel_by_events": dom_events,
                 "op_frac": round((fwd_b + bwd_b) / (ms_per_step * 1e-3 / world) / 1e9 / HBM_PEAK_GBS, 4)}
     # the op's algorithmic bytes over each pass's kernel time (fwd = setup + raster, bwd =
     # grad), and the measured HBM bytes (rocprof PMC, traffic.json) of the dominant kernel over its time --
@@ -345,7 +361,7 @@ def main():
     if t_bwd > 0:
         roofline["bwd_frac"] = round(bwd_b / (t_bwd * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     if traffic is not None:
-        roofline["traffic_frac"] = round(traffic / (kern_us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        roofline["traffic_frac"] = round(traffic / (dur_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     if pass_us:
         # the same fractions on the passes' in-graph times (no launch gap; the roofline above stays on the
         # conservative eager event times)

@@ -195,7 +195,6 @@ int validate(int B, int H, int W, int C, int V, int F)
 #include "setup_kernel.h"
 #include "raster_kernel.h"
 #include "grad_kernel.h"
-#include "grad_persist.h"
 #include "lighting_kernels.h"
 
 // zero two float arrays in one launch (the backward's atomically accumulated outputs)
@@ -349,18 +348,32 @@ int dirt_workspace_sizes(int B, int H, int W, int C, int V, int F, int64_t bin_c
 }  // extern "C"
 
 // Automatic deep-scene culling: the Gouraud raster counts its long per-wave entry lists
-// (raster_kernel deep_host), and the next launch on the same scratch reports whether that count made the launch deep
-// by writing its generation into a host-mapped word per device.  A forward takes the occluder-culling
-// instantiation (OCC) when a launch within the last kDeepRecent generations was deep: a deep scene switches after
-// one launch (plus the queue's lag), a scene turning shallow switches back after kDeepRecent.  Both instantiations are
-// exact, so the choice changes time only.  DIRT_FWD_DEEP_CULL forces OCC, DIRT_FWD_DEEP_CULL_OFF the plain raster;
+// (raster_kernel deep_host) into one of two count slots of its scratch's flag area, and the next launch on the same
+// scratch reports whether that count made the previous launch deep, by writing the previous launch's generation into
+// a host-mapped word per device, then clears that slot.  A forward takes the occluder-culling instantiation (OCC)
+// when a launch within the last kDeepRecent generations was deep: a deep scene switches after one launch (plus the
+// queue's lag), a scene turning shallow switches back after kDeepRecent.  Both instantiations are exact, so the
+// choice changes time only.  DIRT_FWD_DEEP_CULL forces OCC, DIRT_FWD_DEEP_CULL_OFF the plain raster;
 // DIRT_DEEP_CULL_AUTO=0 disables the rule.
-// A stream under graph capture uses the word only once it exists (no allocation during a capture).
+// Per scratch, the host remembers the generation and count slot of the last launch on it, so
+// launches on several scratches interleaved on one device (two layouts, streams or sessions) each report their own
+// previous launch; a launch counts into the slot its predecessor on that scratch did not use.  A launch captured
+// into a graph neither counts nor reports (its instantiation is fixed at capture; replays would re-count into one
+// slot forever), and the word is allocated outside any capture (relaxed capture mode, so another
+// thread's global-mode capture is not invalidated by the host allocation).
 constexpr uint32_t kDeepRecent = 8;
+struct DeepScratch {
+    const void *flag = nullptr;  // the scratch's flag area (identifies the scratch)
+    uint32_t gen = 0;            // generation of the last launch on it
+    uint32_t slot = 0;           // the count slot that launch used
+};
+constexpr int kDeepScratches = 64;
 struct DeepAuto {
     uint32_t *host = nullptr;  // host-mapped word: generation of the last launch reported deep (0 = none)
     uint32_t *dev = nullptr;   // its device address
     uint32_t gen = 0;          // launches issued with the rule on
+    DeepScratch scr[kDeepScratches];  // recently used scratches (round-robin replacement)
+    int next = 0;
 };
 static std::mutex g_deep_mu;
 static DeepAuto g_deep[64];
@@ -375,8 +388,8 @@ static bool deep_auto_enabled()
     return v != 0;
 }
 
-// the device's state with its word allocated (nullptr: rule off or no word yet and the stream is capturing)
-static DeepAuto *deep_auto_state(hipStream_t stream)
+// the device's state with its word allocated (nullptr: rule off or the allocation failed)
+static DeepAuto *deep_auto_state()
 {
     if (!deep_auto_enabled()) return nullptr;
     int dev = 0;
@@ -384,18 +397,33 @@ static DeepAuto *deep_auto_state(hipStream_t stream)
     DeepAuto &d = g_deep[dev];
     std::lock_guard<std::mutex> lk(g_deep_mu);
     if (d.host) return &d;
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    // (relaxed capture mode for this thread: a host allocation is an unsafe call while any stream captures in
+    // global mode, torch.cuda.graph's default)
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
     void *h = nullptr, *dp = nullptr;
-    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
-    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
+    bool ok = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+    if (ok && hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
         (void)hipHostFree(h);
-        return nullptr;
+        ok = false;
     }
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (!ok) return nullptr;
     static_cast<volatile uint32_t *>(h)[0] = 0u;
     d.dev = static_cast<uint32_t *>(dp);
     d.host = static_cast<uint32_t *>(h);
     return &d;
+}
+
+// the record of `flag`'s scratch (created on first use: no previous launch, generation 0); g_deep_mu held
+static DeepScratch &deep_scratch(DeepAuto &d, const void *flag)
+{
+    for (DeepScratch &e : d.scr)
+        if (e.flag == flag) return e;
+    DeepScratch &e = d.scr[d.next];
+    d.next = (d.next + 1) % kDeepScratches;
+    e = DeepScratch{flag, 0u, 0u};
+    return e;
 }
 
 // the forward of every op; tcb = channels of `background` (== C except for hill's terrain lookup)
@@ -452,21 +480,27 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
     // occluder culling of long per-wave entry lists (deep scenes, raster_kernel.h OCC): forced by DIRT_FWD_DEEP_CULL,
     // else automatic (DeepAuto) for the binned Gouraud forward
     bool deep = (flags & DIRT_FWD_DEEP_CULL) != 0 && shader_id == DIRT_SHADER_GOURAUD && !nopix;
-    uint32_t *deep_host = nullptr, deep_gen = 0;
+    DeepArgs dga{};
     if (shader_id == DIRT_SHADER_GOURAUD && !nopix && !fused && !want_gb && F > 0 && !(flags & DIRT_FWD_DEEP_CULL_OFF)) {
-        if (DeepAuto *da = deep_auto_state(stream)) {
-            // (a launch captured into a graph does not count as a generation: it does not execute now, and a long
-            // capture would otherwise age the device's last report past kDeepRecent; its replays repeat the
-            // generation of the capture)
+        if (DeepAuto *da = deep_auto_state()) {
+            // (a launch captured into a graph neither counts nor reports, nor does it advance the generation: it
+            // does not execute now, and its replays keep the instantiation chosen here)
             hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
             const bool capturing = hipStreamIsCapturing(stream, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
             std::lock_guard<std::mutex> lk(g_deep_mu);
-            if (!capturing) ++da->gen;
-            if (da->gen == 0) da->gen = 1;  // (0 means "never deep")
-            deep_gen = da->gen;
             const uint32_t last = static_cast<volatile uint32_t *>(da->host)[0];
-            deep = deep || (last != 0u && deep_gen - last <= kDeepRecent);
-            deep_host = da->dev;
+            const uint32_t next_gen = da->gen + 1u == 0u ? 1u : da->gen + 1u;  // (0 means "never deep")
+            deep = deep || (last != 0u && next_gen - last <= kDeepRecent);
+            if (!capturing) {
+                da->gen = next_gen;
+                DeepScratch &ds = deep_scratch(*da, flag);
+                dga.host = da->dev;
+                dga.gen = next_gen;
+                dga.prev_gen = ds.gen;
+                dga.slot = ds.slot ^ 1u;
+                ds.gen = next_gen;
+                ds.slot = dga.slot;
+            }
         }
     }
     if (F > 0 && !fused) {
@@ -514,7 +548,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
             L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, covbits, zero_grad_vertices,                     \
             zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                  \
             zero_grad_vertex_colors ? (int64_t)B * V * C : 0, vertices, camera_pos, shader_id, tcb, GbufOut{},      \
-            nullptr, nullptr, deep_host, deep_gen);                                                              \
+            nullptr, nullptr, dga);                                                                              \
     else if (fused && want_gb)                                                                                   \
         raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, true, true><<<grid, dim3(256), 0, stream>>>(                   \
             background, vertex_colors, recs, fdata, ccount, flag, bins, L.slab, B, H, W, C, V, F, tile_grid(L.ntx), \
@@ -543,7 +577,7 @@ static int rasterise_fwd_impl(const float *background, int tcb, const float *ver
                                                       zero_grad_vertex_colors,                                     \
                                                       zero_grad_vertex_colors ? (int64_t)B * V * C : 0,            \
                                                       vertices, camera_pos, shader_id, tcb, GbufOut{}, nullptr,    \
-                                                      nullptr, deep_host, deep_gen)
+                                                      nullptr, dga)
     if (C == 1) LAUNCH_RASTER(1);
     else if (C == 3) LAUNCH_RASTER(3);
     else if (C == 7) LAUNCH_RASTER(7);
@@ -588,30 +622,6 @@ int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *verti
     return rasterise_fwd_impl(terrain, terrain_channels, vertices, nullptr, faces, camera_pos, B, H, W, C, V, F,
                               DIRT_SHADER_HILL, pixels, gbuffer, saved, saved_bytes, scratch, scratch_bytes,
                               bin_capacity, 0u, nullptr, nullptr, stream_);
-}
-
-// compute units of the current device (cached per device)
-static int device_cus()
-{
-    static int cache[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (cache[dev] == 0) {
-        int n = 0;
-        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
-    }
-    return cache[dev];
-}
-
-// DIRT_GRAD_PERSIST: workgroups per CU of the persistent backward (0 / unset = the one-tile-per-workgroup grid)
-static int grad_persist_wgs_per_cu()
-{
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("DIRT_GRAD_PERSIST");
-        v = e ? std::max(0, atoi(e)) : 0;
-    }
-    return v;
 }
 
 static NdcScale ndc_scale(int W, int H)
@@ -668,19 +678,6 @@ static int rasterise_bwd_impl(const float *vertices, const float *vertex_colors,
     const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(C) - 1) / grad_tile_h(C);
     dim3 grid((unsigned)(gntx * gnty), (unsigned)B);
     ProfScope ps(K_GRAD, stream);
-    // persistent backward (grad_kernel PERSIST): workgroups per CU from DIRT_GRAD_PERSIST (0 = off), RGB with both
-    // gradients, when the batch has more tiles than that many workgroups
-    const int64_t gtiles = (int64_t)gntx * gnty * B;
-    const int pwpc = grad_persist_wgs_per_cu();
-    if (pwpc > 0 && C == 3 && gm == 3 && kGradTileW == 16 && gtiles > (int64_t)pwpc * device_cus()) {
-        const unsigned nwg = (unsigned)std::min<int64_t>(gtiles, (int64_t)pwpc * device_cus());
-        grad_kernel_persist<3, 0, kGradTileW, grad_tile_h(3), 3><<<dim3(nwg), dim3(GradGeom<kGradTileW, grad_tile_h(3)>::NT),
-                                                                0, stream>>>(
-            pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx), L.nrec,
-            grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H), gntx * gnty, stash_flip);
-        HIP_TRY(hipGetLastError());
-        return DIRT_OK;
-    }
 #define LAUNCH_GRAD_GM(CC, GMV)                                                                              \
     grad_kernel<CC, 0, kGradTileW, grad_tile_h(CC), GMV><<<grid, dim3(GradGeom<kGradTileW, grad_tile_h(CC)>::NT), 0, \
                                                           stream>>>(                                            \

@@ -512,6 +512,15 @@ constexpr int kFusedMaxF = 32;
 #endif
 constexpr int64_t kFusedMaxTiles = DIRT_FUSED_MAX_TILES;
 
+// Automatic deep-scene culling (dirt_raster.hip DeepAuto): `host` null = off.  Sampled workgroups count long lists
+// into count slot `slot` of the scratch's flag area; the first workgroup reports the previous launch on this scratch
+// (generation `prev_gen`, 0 = none, which counted into slot ^ 1) to the host-mapped word if it was deep, then
+// clears that slot.
+struct DeepArgs {
+    uint32_t *host;
+    uint32_t gen, prev_gen, slot;
+};
+
 // NOPIX (Gouraud): coverage-only resolve for dirt_rasterise_bwd_recompute -- the g-buffer and the
 // neighbour-coverage bits the backward reads, no pixels (no background or colour loads, no pixel stores).
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false, bool NOPIX = false,
@@ -529,7 +538,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      int sid, int tcb, GbufOut gbo = GbufOut{},
                                                      const int32_t *__restrict__ faces = nullptr,
                                                      const uint32_t *__restrict__ stash_hdr = nullptr,
-                                                     uint32_t *__restrict__ deep_host = nullptr, uint32_t deep_gen = 0)
+                                                     const DeepArgs dga = DeepArgs{})
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     static_assert(!(GB && kNoDepth), "hill has no depth buffer");
@@ -638,13 +647,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const uint32_t raw = FUSED ? 0xffffffffu
                                : F > 0 ? counts[cc * kCountStride] + counts[((int64_t)B * ncoarse + cc) * kCountStride] : 0u;
     if (!FUSED && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
-    if (deep_host != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {
+    if (dga.host != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {
         // automatic deep culling: report whether the previous launch on this scratch was deep (to the host-mapped
         // word the host reads when it picks the next launch's instantiation), then clear its count slot
-        uint32_t *prev = &flag[kDeepCnt + 4 * ((deep_gen ^ 1u) & 1u)];
+        uint32_t *prev = &flag[kDeepCnt + 4 * (dga.slot ^ 1u)];
         const uint32_t sampled = gridDim.y * ((gridDim.x + kDeepSample - 1) / kDeepSample);
-        if (*prev >= max(1u, sampled / kDeepFrac))
-            __hip_atomic_store(deep_host, deep_gen - 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (dga.prev_gen != 0u && *prev >= max(1u, sampled / kDeepFrac))
+            __hip_atomic_store(dga.host, dga.prev_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         *prev = 0u;
     }
     if (!(AB & 16)) {
@@ -771,9 +780,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                     if (lane == 0) t_wl[wave][ns] = 256u * sizeof(StripEntry);  // pad / sentinel
                     // automatic deep culling: one workgroup in kDeepSample counts the long lists of its wave 0 (one
                     // non-returning atomic per such staging round: the counter is a single word)
-                    if (deep_host != nullptr && wave == 0 && lane == 0 && (blockIdx.x & (kDeepSample - 1)) == 0 &&
+                    if (dga.host != nullptr && wave == 0 && lane == 0 && (blockIdx.x & (kDeepSample - 1)) == 0 &&
                         ns > kDeepMark)
-                        atomicAdd(&flag[kDeepCnt + 4 * (deep_gen & 1u)], 1u);
+                        atomicAdd(&flag[kDeepCnt + 4 * dga.slot], 1u);
                     wave_lds_sync();
                     // two entries per iteration; the next pair's offsets are read before this pair is
                     // tested (reads at k + 2 <= ns + 1 stay inside the list)

@@ -30,10 +30,10 @@ static_assert(kMaxClipVerts - 2 == kExtraPerFace + 1, "sub-triangle slots");
 // fixed polygon buffer and clips in higher precision), so these count where this rasteriser's output may differ
 // from the reference's for reasons other than driver arithmetic.  Only the clipping slow path touches them.
 constexpr int kStatCapCulled = 48, kStatClamped = 52;
-// Automatic deep-scene culling (raster_kernel deep_host): per launch, the number of sampled workgroups (one in
-// kDeepSample) whose wave 0 found more than kDeepMark entries in its first list, in two slots by launch-generation
-// parity (words kDeepCnt, kDeepCnt + 4).  A launch zeroes the previous generation's slot after reporting it; a launch
-// is deep when at least 1 / kDeepFrac of the sampled workgroups marked it.
+// Automatic deep-scene culling (raster_kernel DeepArgs): per launch, the number of sampled workgroups (one in
+// kDeepSample) whose wave 0 found more than kDeepMark entries in its first list, in two slots that alternate between
+// the launches on one scratch (words kDeepCnt, kDeepCnt + 4).  A launch zeroes its predecessor's slot after reporting
+// it; a launch is deep when at least 1 / kDeepFrac of the sampled workgroups marked it.
 constexpr int kDeepCnt = 56;
 constexpr int kDeepMark = 64;
 constexpr uint32_t kDeepSample = 16, kDeepFrac = 8;

@@ -83,12 +83,13 @@ void init(const std::string &path)
 
 // Forward-only scratch (bins, bin counters) per (device, stream, layout), cleared once: every forward
 // leaves it clean for the next one of the same layout (DIRT_FWD_SCRATCH_CLEAN).  LRU of a few layouts.
-// Graph capture (ADVICE r4): a scratch created while the stream captures a HIP graph comes from that graph's
-// private memory pool and is cleared by a memset captured into the graph, i.e. it is clean only for that graph's
-// replays.  Those entries are keyed by the capture id too (dirt_stream_capture_id) and kept apart: forwards of
-// one capture share one, no other capture or eager call sees it, and dropping the cache's reference is safe at
-// any time (the block stays in the graph's pool).  An entry whose forward failed is discarded (its alternating
-// count sets may be dirty).  The Python twin is dirt_amd.rasterise_ops._Workspace.
+// Graph capture (ADVICE r4, r5): a scratch created while the stream captures a HIP graph comes from that graph's
+// memory pool and is cleared by a kernel captured into the graph, i.e. it is clean only for that graph's replays.
+// Those entries are keyed by the capture id too (dirt_stream_capture_id): forwards of one capture share one, no
+// other capture or eager call sees it, and they stay PINNED until clear(force = true) -- the graph writes them at
+// every replay, and a block released to a pool that a later capture shares (torch.cuda.graph(pool=...),
+// make_graphed_callables) could otherwise be handed to that capture too.  An entry whose forward failed is
+// discarded (its alternating count sets may be dirty).  The Python twin is dirt_amd.rasterise_ops._CaptureKeyedCache.
 struct ScratchCache {
     typedef std::tuple<int, uintptr_t, int64_t, int64_t, int64_t, int64_t, int64_t> Key;
     struct Entry {
@@ -96,9 +97,8 @@ struct ScratchCache {
         at::Tensor t;
     };
     std::mutex mu;
-    std::list<Entry> lru;             // eager entries
-    unsigned long long cap_id = 0;    // the capture the entries below belong to
-    std::list<Entry> cap;
+    std::list<Entry> lru;                                  // eager entries
+    std::map<unsigned long long, std::list<Entry>> caps;  // capture id -> its entries (pinned)
     static unsigned long long capture_id(hipStream_t stream)
     {
         hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -127,11 +127,7 @@ struct ScratchCache {
         const unsigned long long cid = capture_id(stream);
         {
             std::lock_guard<std::mutex> g(mu);
-            if (cid && cid != cap_id) {  // a new capture: the previous one's entries belong to its graph now
-                cap_id = cid;
-                cap.clear();
-            }
-            if (at::Tensor *t = find(cid ? cap : lru, k, !cid)) {
+            if (at::Tensor *t = find(cid ? caps[cid] : lru, k, !cid)) {
                 if (debug()) fprintf(stderr, "[dirt scratch] hit stream %p capture %llu ptr %p\n", (void *)stream, cid, t->data_ptr());
                 return *t;
             }
@@ -142,7 +138,7 @@ struct ScratchCache {
                                   std::get<6>(k), t.data_ptr(), bytes, stream));
         std::lock_guard<std::mutex> g(mu);
         if (cid) {
-            if (cid == cap_id) cap.push_front(Entry{k, t});
+            caps[cid].push_front(Entry{k, t});
         } else {
             lru.push_front(Entry{k, t});
             while (lru.size() > 4) lru.pop_back();
@@ -153,18 +149,21 @@ struct ScratchCache {
     {
         std::lock_guard<std::mutex> g(mu);
         lru.remove_if([&](const Entry &e) { return e.key == k; });
-        cap.remove_if([&](const Entry &e) { return e.key == k; });
+        for (auto &c : caps) c.second.remove_if([&](const Entry &e) { return e.key == k; });
     }
-    void clear(bool)
+    // eager entries; `force`: the captures' pinned entries too (once their graphs are destroyed)
+    void clear(bool force)
     {
         std::lock_guard<std::mutex> g(mu);
         lru.clear();
-        cap.clear();
+        if (force) caps.clear();
     }
     size_t size()
     {
         std::lock_guard<std::mutex> g(mu);
-        return lru.size() + cap.size();
+        size_t n = lru.size();
+        for (auto &c : caps) n += c.second.size();
+        return n;
     }
 } g_scratch;
 

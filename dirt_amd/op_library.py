@@ -23,7 +23,8 @@ recomputation): it is the faster path; this module is the drop-in boundary the n
 import torch
 
 from . import _lib
-from .rasterise_ops import _as_tensor, _camera, _check_shapes, _device_of, _on_device, _upstream_positional
+from .rasterise_ops import (_as_tensor, _camera, _CaptureKeyedCache, _check_shapes, _device_of, _on_device,
+                            _upstream_positional)
 
 __all__ = ["load_op_library", "RasteriseOpModule"]
 
@@ -40,66 +41,47 @@ class _RasteriseSingleOutput(torch.autograd.Function):
         with _on_device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             nbytes = _lib.recompute_workspace_size(B, H, W, C, V, F)
-            ws = _stash_workspaces.get(dev, stream, (B, H, W, C, V, F), nbytes)
+            layout = (B, H, W, C, V, F)
+            ws = _stash_workspaces.get(dev, stream, layout, nbytes)
             # (camera_pos is read by the procedural programs only; Gouraud ignores it)
-            _lib.check(lib.dirt_rasterise_fwd_stash(
-                background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
-                B, H, W, C, V, F, pixels.data_ptr(), ws.data_ptr(), nbytes, _lib.FWD_SCRATCH_CLEAN, stream))
+            try:
+                _lib.check(lib.dirt_rasterise_fwd_stash(
+                    background.data_ptr(), vertices.data_ptr(), vertex_colors.data_ptr(), faces.data_ptr(),
+                    B, H, W, C, V, F, pixels.data_ptr(), ws.data_ptr(), nbytes, _lib.FWD_SCRATCH_CLEAN, stream))
+            except Exception:
+                _stash_workspaces.discard(dev, stream, layout)  # its bin counters may be dirty now
+                raise
         # what TF hands a registered gradient: op.inputs and op.outputs (+ the op's workspace resource)
         ctx.save_for_backward(background, vertices, vertex_colors, faces, pixels)
         ctx.dims = (B, H, W, C, V, F)
         ctx.workspace = ws
+        ctx.ws_key = (dev, stream, layout)
         return pixels
 
     @staticmethod
     def backward(ctx, grad_pixels):
         background, vertices, vertex_colors, faces, pixels = ctx.saved_tensors
-        return rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, ctx.dims,
-                                        workspace=ctx.workspace) + (None,) * 5
+        try:
+            grads = rasterise_grad_recompute(background, vertices, vertex_colors, faces, pixels, grad_pixels, ctx.dims,
+                                             workspace=ctx.workspace)
+        except Exception:
+            _stash_workspaces.discard(*ctx.ws_key)
+            raise
+        return grads + (None,) * 5
 
 
-class _StashWorkspaces:
+def _make_stash_workspace(nbytes, dev, stream, layout):
+    return torch.zeros((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+
+
+class _StashWorkspaces(_CaptureKeyedCache):
     """Zero-filled recompute workspaces per (device, stream, layout[, capture id]), LRU of a few layouts.  Every
     forward-stash and recompute leaves one clean (DIRT_BWD_SCRATCH_CLEAN); a capture gets workspaces of its own
-    (allocated in its graph's pool, zero-filled by a captured memset), as rasterise_ops._Workspace."""
+    (allocated in its graph's pool, zero-filled by a captured kernel), pinned for the graph's lifetime, as
+    rasterise_ops._Workspace.  A workspace whose call failed is dropped (`discard`)."""
 
     def __init__(self, keep=4):
-        import collections
-        import threading
-        self.keep = keep
-        self._lock = threading.Lock()
-        self._d = collections.OrderedDict()
-        self._cap_id, self._cap = 0, {}
-
-    def get(self, dev, stream, layout, nbytes):
-        cid = _lib.capture_id(stream) if torch.cuda.is_current_stream_capturing() else 0
-        key = (dev, stream, layout)
-        with self._lock:
-            if cid:
-                if cid != self._cap_id:
-                    self._cap_id, self._cap = cid, {}
-                t = self._cap.get(key)
-            else:
-                t = self._d.get(key)
-                if t is not None:
-                    self._d.move_to_end(key)
-            if t is not None:
-                return t
-        t = torch.zeros((max(nbytes, 1),), dtype=torch.uint8, device=dev)
-        with self._lock:
-            if cid:
-                if cid == self._cap_id:
-                    self._cap[key] = t
-            else:
-                self._d[key] = t
-                while len(self._d) > self.keep:
-                    self._d.popitem(last=False)
-        return t
-
-    def clear(self):
-        with self._lock:
-            self._d.clear()
-            self._cap = {}
+        super().__init__(_make_stash_workspace, keep)
 
 
 _stash_workspaces = _StashWorkspaces()

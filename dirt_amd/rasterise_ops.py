@@ -66,39 +66,30 @@ class _on_device:
 _DEBUG_SCRATCH = os.environ.get("DIRT_DEBUG_SCRATCH") is not None
 
 
-class _Workspace:
-    """Per-(device, stream, layout) cache of the forward-only scratch (tile bins, bin counters).
+class _CaptureKeyedCache:
+    """Device buffers per (device, stream, layout), with graph captures kept apart.
 
-    A scratch zero-filled once stays clean across forwards of the same layout (the bin counters alternate
-    between two sets, include/dirt_mi355x.h DIRT_FWD_SCRATCH_CLEAN), so a cached one saves every call the
-    counter memset (128 MiB for B = 64 at 8192^2 with one 256-B line per counter) and the allocation.
-    Keyed by the stream too: two streams never share a scratch.  A few layouts are kept (LRU).
+    Eager entries: an LRU of `keep` layouts.  An entry made while its stream captures a HIP graph comes from that
+    graph's memory pool and is initialised by nodes of that graph, so it is valid only for that graph's replays:
+    such entries are keyed by the capture id as well (`dirt_stream_capture_id`), no other capture or eager call
+    ever sees one, and they are PINNED -- kept referenced until `clear(force=True)` -- because the graph goes on
+    writing them at every replay.  Dropping the reference early would return the block to the pool, and a later
+    capture sharing that pool (`torch.cuda.graph(..., pool=...)`, `make_graphed_callables`) could be handed the
+    same memory: two graphs writing one buffer.  `make(nbytes, dev, stream)` creates a buffer."""
 
-    Graph capture: a scratch created while a stream captures a HIP graph is allocated from that
-    graph's private memory pool and cleared by a memset captured into that graph, so it is clean only for that
-    graph's replays.  Such entries are keyed by the capture id as well (`dirt_stream_capture_id`): forwards of
-    one capture share one scratch, and no other capture or eager call ever sees it (a second graph of the same
-    layout gets its own, cleared by its own replays -- whichever graph replays first).  Eager entries are never
-    handed to a capture either.  Dropping the cache's reference to a capture's scratch is safe at any time: the
-    block stays in the graph's private pool, which only that graph's replays use.  An entry whose forward
-    failed after its first launch is dropped (`discard`): its alternating bin-count sets may no longer be
-    clean."""
-
-    def __init__(self, keep=4):
+    def __init__(self, make, keep=4):
         self.keep = keep
+        self._make = make
         self._lock = threading.Lock()
         self._d = collections.OrderedDict()
-        self._cap_id = 0
-        self._cap = {}
+        self._caps = {}  # capture id -> {key: tensor}, pinned
 
-    def scratch(self, dev, stream, layout, nbytes):
+    def get(self, dev, stream, layout, nbytes):
         cid = _lib.capture_id(stream) if torch.cuda.is_current_stream_capturing() else 0
         key = (dev, stream, layout)
         with self._lock:
             if cid:
-                if cid != self._cap_id:  # a new capture: the previous one's entries are its graph's now
-                    self._cap_id, self._cap = cid, {}
-                t = self._cap.get(key)
+                t = self._caps.get(cid, {}).get(key)
             else:
                 t = self._d.get(key)
                 if t is not None:
@@ -107,17 +98,12 @@ class _Workspace:
                 if _DEBUG_SCRATCH:
                     print("[dirt scratch py] hit stream %x capture %d ptr %x" % (stream, cid, t.data_ptr()), file=sys.stderr)
                 return t
-        # only the bin counters need zeroing (dirt_scratch_clear: a memset of the counter lines); the slabs
-        # are written before they are read.  Under capture the memset is part of the graph.
-        t = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+        t = self._make(nbytes, dev, stream, layout)
         if _DEBUG_SCRATCH:
             print("[dirt scratch py] new stream %x capture %d ptr %x" % (stream, cid, t.data_ptr()), file=sys.stderr)
-        B, H, W, F, cap = layout
-        _lib.check(_lib.load().dirt_scratch_clear(B, H, W, F, cap, t.data_ptr(), nbytes, stream))
         with self._lock:
             if cid:
-                if cid == self._cap_id:
-                    self._cap[key] = t
+                self._caps.setdefault(cid, {})[key] = t
             else:
                 self._d[key] = t
                 while len(self._d) > self.keep:
@@ -125,21 +111,51 @@ class _Workspace:
         return t
 
     def discard(self, dev, stream, layout):
+        """Drop an entry whose call failed after its first launch (its state may no longer be clean).  A capture's
+        entry is dropped too: the failed capture is invalid anyway."""
+        key = (dev, stream, layout)
         with self._lock:
-            key = (dev, stream, layout)
             self._d.pop(key, None)
-            self._cap.pop(key, None)
+            for m in self._caps.values():
+                m.pop(key, None)
 
     def clear(self, force=False):
-        """Drop every cached scratch (`force` is accepted for compatibility: graph-owned scratch lives in its
-        graph's memory pool, so nothing needs pinning)."""
+        """Drop the eager entries; `force` also unpins the graph captures' entries (call it once the graphs that
+        were captured through the op are destroyed)."""
         with self._lock:
             self._d.clear()
-            self._cap = {}
+            if force:
+                self._caps = {}
 
     def __len__(self):
         with self._lock:
-            return len(self._d) + len(self._cap)
+            return len(self._d) + sum(len(m) for m in self._caps.values())
+
+
+def _make_scratch(nbytes, dev, stream, layout):
+    # only the bin counters need zeroing (dirt_scratch_clear: a kernel over the counter lines); the slabs are
+    # written before they are read.  Under capture the clear is a node of the graph.
+    t = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    B, H, W, F, cap = layout
+    _lib.check(_lib.load().dirt_scratch_clear(B, H, W, F, cap, t.data_ptr(), nbytes, stream))
+    return t
+
+
+class _Workspace(_CaptureKeyedCache):
+    """Per-(device, stream, layout) cache of the forward-only scratch (tile bins, bin counters).
+
+    A scratch zero-filled once stays clean across forwards of the same layout (the bin counters alternate
+    between two sets, include/dirt_mi355x.h DIRT_FWD_SCRATCH_CLEAN), so a cached one saves every call the
+    counter clear (128 MiB for B = 64 at 8192^2 with one 256-B line per counter) and the allocation.
+    Keyed by the stream too: two streams never share a scratch.  Graph captures get scratch of their own,
+    pinned for the graphs' lifetime (_CaptureKeyedCache).  An entry whose forward failed after its first launch
+    is dropped (`discard`): its alternating bin-count sets may no longer be clean."""
+
+    def __init__(self, keep=4):
+        super().__init__(_make_scratch, keep)
+
+    def scratch(self, dev, stream, layout, nbytes):
+        return self.get(dev, stream, layout, nbytes)
 
 
 _workspace = _Workspace()
@@ -343,9 +359,12 @@ def _torch_ext():
 
 
 def workspace_cache_clear(force=False):
-    """Drop the cached per-layout scratch buffers (both implementations).  Graphs captured through the op keep
-    working: their scratch lives in the graph's own memory pool (`force` is accepted for compatibility)."""
+    """Drop the cached per-layout scratch buffers (both implementations) and the single-output op's workspaces.
+    Scratch made inside a graph capture stays pinned (its graph writes it at every replay) unless `force`: call
+    `workspace_cache_clear(force=True)` once the graphs captured through the op are destroyed."""
     _workspace.clear(force)
+    from . import op_library
+    op_library._stash_workspaces.clear(force)
     ext = _torch_ext()
     if ext is not None:
         ext.scratch_cache_clear(bool(force))

@@ -281,12 +281,18 @@ def test_captured_graph_survives_cache_eviction_and_clear(impl):
     assert rasterise_ops.workspace_cache_size() == 0
 
 
+@pytest.mark.filterwarnings("error:The AccumulateGrad node's stream does not match")
+@pytest.mark.parametrize("shared_pool", [False, True])
 @pytest.mark.parametrize("impl", ["ext", "py"])
-def test_two_graphs_same_layout_second_replayed_first(impl):
+def test_two_graphs_same_layout_second_replayed_first(impl, shared_pool):
     """two graphs captured through the public op with the same layout (torch.cuda.graph's default
     capture stream, so the same (device, stream, layout) key) must not share a scratch created inside the
     first capture: that scratch is cleared only by the first graph's replays.  Replay the second graph before
-    the first has ever run, on a dirtied allocator, and compare both with the eager results."""
+    the first has ever run, on a dirtied allocator, and compare both with the eager results.
+    shared_pool: the second graph is captured into the first one's memory pool
+    (torch.cuda.graph(..., pool=first.pool())), so a scratch of the first capture that the op's cache released
+    could be handed to the second capture; the graphs are then replayed interleaved in capture order (the order
+    torch requires of graphs sharing a pool), every output checked after every replay."""
     from dirt_amd import rasterise_ops
     ext = rasterise_ops._torch_ext()
     if impl == "ext":
@@ -309,14 +315,14 @@ def test_two_graphs_same_layout_second_replayed_first(impl):
         ft = _gpu(f)
         g = torch.randn(bg.shape, device="cuda")
         keep.append((t, ft, g))  # a graph's inputs must outlive it (the loop rebinds t, ft, g)
-        # (the eager reference on a side stream: an eager fwd + autograd backward of the op on the legacy default
-        # stream before a capture on another stream segfaulted in torch's capture_end on this stack --
-        # tools/debug/capture_repro2.py)
-        s_ = torch.cuda.Stream()
-        s_.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s_):
-            px, _ = op(t[0], t[1], t[2], ft, H, W, C)
-            refs.append((px.detach().clone(), [x.clone() for x in torch.autograd.grad(px, t, g)]))
+        # the eager reference on the legacy default stream, the pattern users write.  Its output is released before
+        # the capture: an autograd graph kept alive keeps the leaves' AccumulateGrad nodes, which remember the
+        # default stream they were made on, and torch's engine then joins the capture stream with the default stream
+        # inside the capture.  That ends in a segfault in torch.cuda.graph's capture_end on this stack with no
+        # dirt_amd code at all (tools/debug/capture_control.py)
+        px, _ = op(t[0], t[1], t[2], ft, H, W, C)
+        refs.append((px.detach().clone(), [x.clone() for x in torch.autograd.grad(px, t, g)]))
+        del px
         torch.cuda.synchronize()
         out = {}
 
@@ -327,23 +333,30 @@ def test_two_graphs_same_layout_second_replayed_first(impl):
 
         # warm-up on a side stream (lazy autograd / allocator initialisation must not happen inside a capture), then
         # capture on torch.cuda.graph's class-wide default capture stream: both graphs share (device, stream, layout)
+        s_ = torch.cuda.Stream()
+        s_.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s_):
             step()
         torch.cuda.current_stream().wait_stream(s_)
         torch.cuda.synchronize()
+        out.clear()  # (the warm-up's autograd graph, made on s_, released before the capture for the same reason)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, pool=graphs[0].pool() if shared_pool and graphs else None):
             step()
         graphs.append(graph)
         outs.append(out)
     torch.cuda.synchronize()
-    for k in (1, 0, 1, 0):
+    ran = set()
+    for k in ((0, 1, 0, 1) if shared_pool else (1, 0, 1, 0)):
         graphs[k].replay()
         torch.cuda.synchronize()
-        assert torch.equal(outs[k]["px"], refs[k][0]), "graph %d: pixels differ from the eager call" % k
-        assert torch.equal(outs[k]["grads"][0], refs[k][1][0])
-        for a, b in zip(outs[k]["grads"][1:], refs[k][1][1:]):
-            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
+        ran.add(k)
+        # (every graph replayed so far: a replay must not disturb another graph's outputs either)
+        for j in sorted(ran):
+            assert torch.equal(outs[j]["px"], refs[j][0]), "graph %d: pixels differ from the eager call" % j
+            assert torch.equal(outs[j]["grads"][0], refs[j][1][0])
+            for a, b in zip(outs[j]["grads"][1:], refs[j][1][1:]):
+                torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()))
     del graphs
     rasterise_ops.workspace_cache_clear(force=True)
 
@@ -351,7 +364,7 @@ def test_two_graphs_same_layout_second_replayed_first(impl):
 def test_captured_scratch_clear_is_ordered_in_the_graph():
     """A scratch created inside a capture is cleared by a node of that graph at every replay.  With the clear as a
     hipMemsetAsync node the bin counters were not clean at the next replay on this stack (they grew by 61,440 per
-    replay, so every tile took the exact but slow all-records path, tools/debug/capture_repro4.py); the clear is a
+    replay, so every tile took the exact but slow all-records path, gpurun logs repro4_*.log of round 5); the clear is a
     kernel since round 5.  Replay a captured forward several times: the fullest slab stays at the eager count."""
     import ctypes
     from dirt_amd import _lib, rasterise_ops
@@ -385,7 +398,7 @@ def test_captured_scratch_clear_is_ordered_in_the_graph():
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         out = fwd()
-    scratch = next(iter(rasterise_ops._workspace._cap.values()))
+    scratch = next(iter(next(iter(rasterise_ops._workspace._caps.values())).values()))
     for _ in range(4):
         graph.replay()
         torch.cuda.synchronize()

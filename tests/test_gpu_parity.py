@@ -512,6 +512,41 @@ def test_deep_cull_automatic_rule():
         np.testing.assert_array_equal(pix, px)
 
 
+def test_deep_cull_rule_with_interleaved_scratches():
+    """forwards on two scratches interleaved on one device (two sessions, one deep scene and one shallow)
+    must each report their own previous launch.  With the count slot chosen by the device's generation parity, the
+    deep session always drew the same parity and read the slot the shallow session used, so it was never reported
+    deep.  Alternate them: the deep launches are reported, the shallow ones are not, and both stay exact."""
+    import torch
+    from dirt_amd import _lib
+    from dirt_amd.session import RasteriseSession
+    deep = tuple(a[None] for a in scenes.random_triangles(F=6000, W=256, H=256, radius_px=64.0, seed=5))
+    shallow = tuple(a[None] for a in scenes.random_triangles(F=4000, W=256, H=192, radius_px=4.0, seed=6))
+    sess = {name: (RasteriseSession(*sc[0].shape, sc[1].shape[1], sc[3].shape[1], device="cuda"), [_gpu(a) for a in sc])
+            for name, sc in (("deep", deep), ("shallow", shallow))}
+    # eight shallow forwards first, so that no earlier test's deep report is recent
+    for _ in range(9):
+        sess["shallow"][0].forward(*sess["shallow"][1])
+    torch.cuda.synchronize()
+    before = _lib.deep_cull_state()
+    assert not before["next_deep"]
+    for _ in range(4):
+        for name in ("deep", "shallow"):
+            s, args = sess[name]
+            s.forward(*args)
+            torch.cuda.synchronize()
+    after = _lib.deep_cull_state()
+    assert after["gen"] == before["gen"] + 8
+    # the deep session's launches are the odd generations after `before`; the last one reported is the third (a launch
+    # is reported by the next launch on its own scratch)
+    assert after["last_deep"] > before["gen"], "the interleaved deep scene's forwards were not reported deep"
+    assert (after["last_deep"] - before["gen"]) % 2 == 1, "a shallow forward was reported deep"
+    for name, sc in (("deep", deep), ("shallow", shallow)):
+        px, gb, _ = oracle.rasterise_fwd(*sc)
+        np.testing.assert_array_equal(sess[name][0].gbuffer.cpu().numpy(), gb)
+        np.testing.assert_array_equal(sess[name][0].pixels.cpu().numpy(), px)
+
+
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DIRT_FUZZ_FIRST", "0")),
                                          int(os.environ.get("DIRT_FUZZ_SEEDS", "36"))))
 def test_fuzz_adversarial_scenes(seed):
