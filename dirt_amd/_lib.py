@@ -27,7 +27,7 @@ SHADER_HILL = 7
 
 MAX_CHANNELS = 8
 MAX_DIM = 8192
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 FWD_SCRATCH_CLEAN = 1  # dirt_rasterise_fwd flags
 FWD_DEEP_CULL = 2      # dirt_rasterise_fwd: occluder culling for deep scenes (forced; automatic since ABI 12)
@@ -49,6 +49,7 @@ SIGNATURES = {
     "dirt_rasterise_fwd_gbuffer": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _U,
                                         _P, _P, _P, _P, _P, _P]),
     "dirt_hill_fwd": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _I64, _P]),
+    "dirt_rasterise_fwd_resolve": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P, _P, _P, _P, _P]),
     "dirt_rasterise_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _U, _P]),
     "dirt_bwd_recompute_workspace_size": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(_SZ)]),
     "dirt_rasterise_bwd_recompute": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _U,

@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void stash_update_kernel(const uint32_t *__res
 
 extern "C" {
 
-int dirt_abi_version(void) { return 12; }
+int dirt_abi_version(void) { return 13; }
 
 const char *dirt_last_error(void) { return g_last_error.c_str(); }
 
@@ -612,6 +612,43 @@ int dirt_rasterise_fwd_gbuffer(const float *background, const float *vertices, c
                               DIRT_SHADER_GOURAUD, pixels, gbuffer, saved, saved_bytes, scratch, scratch_bytes,
                               bin_capacity, flags, zero_grad_vertices, zero_grad_vertex_colors, stream_,
                               GbufOut{depth, barycentrics, face_ids});
+}
+
+// A render sharing its geometry with the earlier Gouraud forward that filled gbuffer_in / saved (ABI 13): the resolve
+// alone, over this render's colours and background (raster_kernel RESOLVE)
+int dirt_rasterise_fwd_resolve(const float *background, const float *vertex_colors, int B, int H, int W, int C, int V,
+                               int F, const int32_t *gbuffer_in, const void *saved, size_t saved_bytes, float *pixels,
+                               int32_t *gbuffer, float *zero_grad_vertices, float *zero_grad_vertex_colors, void *stream_)
+{
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    if (B == 0) return DIRT_OK;
+    if (!background || !pixels || !gbuffer || !gbuffer_in || !saved || (V > 0 && !vertex_colors))
+        return fail(DIRT_EINVAL, "RasteriseResolve: null tensor pointer");
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    if (saved_bytes < L.saved_total) return fail(DIRT_EINVAL, "RasteriseResolve: saved smaller than dirt_workspace_sizes()");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const char *sv = static_cast<const char *>(saved);
+    const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
+    const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    dim3 grid((unsigned)L.ntiles, (unsigned)B);
+    ProfScope ps(K_RASTER, stream);
+#define LAUNCH_RESOLVE(CC)                                                                                         \
+    raster_kernel<CC, 0, DIRT_SHADER_GOURAUD, false, false, false, false, true><<<grid, dim3(256), 0, stream>>>(     \
+        background, vertex_colors, recs, fdata, nullptr, nullptr, nullptr, 0u, B, H, W, C, V, F, tile_grid(L.ntx),   \
+        L.cshift, L.nctx, L.ncoarse, L.nrec, pixels, gbuffer, nullptr, zero_grad_vertices,                        \
+        zero_grad_vertices ? (int64_t)B * V * 4 : 0, zero_grad_vertex_colors,                                     \
+        zero_grad_vertex_colors ? (int64_t)B * V * C : 0, nullptr, nullptr, DIRT_SHADER_GOURAUD, C, GbufOut{},      \
+        nullptr, nullptr, DeepArgs{}, gbuffer_in)
+    if (C == 1) LAUNCH_RESOLVE(1);
+    else if (C == 3) LAUNCH_RESOLVE(3);
+    else if (C == 7) LAUNCH_RESOLVE(7);
+    else LAUNCH_RESOLVE(0);
+#undef LAUNCH_RESOLVE
+    HIP_TRY(hipGetLastError());
+    return DIRT_OK;
 }
 
 int dirt_hill_fwd(const float *terrain, int terrain_channels, const float *vertices, const int32_t *faces,

@@ -524,7 +524,7 @@ struct DeepArgs {
 // NOPIX (Gouraud): coverage-only resolve for dirt_rasterise_bwd_recompute -- the g-buffer and the
 // neighbour-coverage bits the backward reads, no pixels (no background or colour loads, no pixel stores).
 template <int CC, int AB = 0, int SH = DIRT_SHADER_GOURAUD, bool GB = false, bool FUSED = false, bool NOPIX = false,
-          bool OCC = false>
+          bool OCC = false, bool RESOLVE = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(SH == DIRT_SHADER_GOURAUD && CC > 0 ? DIRT_RASTER_WAVES : 1))) DIRT_RASTER_ATTR void raster_kernel(const float *__restrict__ background, const float *__restrict__ colors,
                                                      const Rec *__restrict__ recs, const FaceData *__restrict__ fdata,
                                                      const uint32_t *__restrict__ counts, uint32_t *__restrict__ flag,
@@ -538,12 +538,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
                                                      int sid, int tcb, GbufOut gbo = GbufOut{},
                                                      const int32_t *__restrict__ faces = nullptr,
                                                      const uint32_t *__restrict__ stash_hdr = nullptr,
-                                                     const DeepArgs dga = DeepArgs{})
+                                                     const DeepArgs dga = DeepArgs{},
+                                                     const int32_t *__restrict__ gb_in = nullptr)
 {
     constexpr bool kNoDepth = SH == DIRT_SHADER_HILL;
     static_assert(!(GB && kNoDepth), "hill has no depth buffer");
     static_assert(!FUSED || SH == DIRT_SHADER_GOURAUD, "the fused small-scene forward is Gouraud only");
     static_assert(!NOPIX || (SH == DIRT_SHADER_GOURAUD && !GB), "the coverage-only resolve is Gouraud only");
+    // RESOLVE (dirt_rasterise_fwd_resolve): a render sharing its geometry with an earlier forward -- no bins, no
+    // visibility pass: the visible record comes from that forward's g-buffer (`gb_in`), the rest is the resolve below,
+    // which then writes this render's own copy of the g-buffer word and leaves the coverage bits alone
+    static_assert(!RESOLVE || (SH == DIRT_SHADER_GOURAUD && !GB && !FUSED && !NOPIX && !OCC), "resolve-only: plain Gouraud");
     // FUSED: the frame's records and FaceData, set up in LDS by this workgroup
     __shared__ Rec s_recs[FUSED ? (1 + kExtraPerFace) * kFusedMaxF : 1];
     __shared__ FaceData s_fd[FUSED ? kFusedMaxF : 1];
@@ -644,9 +649,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     // This forward's setup zeroed the other count set, so the count is the sum of both (no dependent
     // parity load); F == 0: setup did not run.  FUSED: no bins (the count sets stay clean), every record
     // of the frame is filtered (the overflow path)
-    const uint32_t raw = FUSED ? 0xffffffffu
+    const uint32_t raw = RESOLVE ? 0u : FUSED ? 0xffffffffu
                                : F > 0 ? counts[cc * kCountStride] + counts[((int64_t)B * ncoarse + cc) * kCountStride] : 0u;
-    if (!FUSED && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
+    if (!FUSED && !RESOLVE && blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && !(AB & 16)) flag[kParQ] = (flag[kParP] & 1u) ^ 1u;
     if (dga.host != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {
         // automatic deep culling: report whether the previous launch on this scratch was deep (to the host-mapped
         // word the host reads when it picks the next launch's instantiation), then clear its count slot
@@ -684,7 +689,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
     const uint32_t rx0 = (uint32_t)(ti0 - (cx << cshift)), rx1 = rx0 + kTile - 1;
     const uint32_t ry0 = (uint32_t)(tj0 - (cy << cshift)), ry1 = ry0 + kTile - 1;
 
-    if (AB & 8) {
+    if (RESOLVE) {
+        // (no visibility pass)
+    } else if (AB & 8) {
         best = raw;
     } else {
         // The workgroup reads its coarse bin once: each wave filters a quarter of every 512-entry chunk
@@ -913,7 +920,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
         gbuffer[o] = (int32_t)best;
         return;
     }
-    const int32_t best_rec = best != kKeyInit<kNoDepth> ? key_rec(key_low<kNoDepth>(best), F) : -1;
+    int32_t best_rec;
+    if constexpr (RESOLVE) {
+        const int32_t g = gb_in[o];
+        best_rec = g >= 0 ? (g & kGbufIndexMask) : -1;
+    } else {
+        best_rec = best != kKeyInit<kNoDepth> ? key_rec(key_low<kNoDepth>(best), F) : -1;
+    }
     if (best_rec < 0) {
         gbuffer[o] = -1;
         if constexpr (GB) {
@@ -925,7 +938,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             }
             if (gbo.face) gbo.face[o] = -1;
         }
-        if constexpr (SH == DIRT_SHADER_GOURAUD) covbits[o] = 0;
+        if constexpr (SH == DIRT_SHADER_GOURAUD && !RESOLVE) covbits[o] = 0;
         if constexpr (!NOPIX) {
 #pragma unroll
             for (int c2 = 0; c2 < CM; ++c2)
@@ -1069,6 +1082,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_
             const float *c0 = cb + (int64_t)fd.v[0] * C, *c1 = cb + (int64_t)fd.v[1] * C, *c2 = cb + (int64_t)fd.v[2] * C;
             for (int k = 0; k < C; ++k) out[k] = (lam[0] * c0[k] + lam[1] * c1[k]) + lam[2] * c2[k];
         }
+        if (!RESOLVE)
         covbits[o] = (AB & 32) ? (uint8_t)0
                                : (uint8_t)neighbour_coverage(rp, E, fd.clipped != 0, best_rec, frame_recs,
                                                              fdata_frame, F, face_of_record(best_rec, F), i, j,

@@ -30,6 +30,7 @@ struct Api {
     decltype(&dirt_workspace_sizes) workspace_sizes = nullptr;
     decltype(&dirt_rasterise_fwd) fwd = nullptr;
     decltype(&dirt_rasterise_fwd_gbuffer) fwd_gbuffer = nullptr;
+    decltype(&dirt_rasterise_fwd_resolve) fwd_resolve = nullptr;
     decltype(&dirt_rasterise_bwd) bwd = nullptr;
     decltype(&dirt_scratch_clear) scratch_clear = nullptr;
     decltype(&dirt_check_faces) check_faces = nullptr;
@@ -66,6 +67,7 @@ void init(const std::string &path)
     g_api.workspace_sizes = reinterpret_cast<decltype(g_api.workspace_sizes)>(sym("dirt_workspace_sizes"));
     g_api.fwd = reinterpret_cast<decltype(g_api.fwd)>(sym("dirt_rasterise_fwd"));
     g_api.fwd_gbuffer = reinterpret_cast<decltype(g_api.fwd_gbuffer)>(sym("dirt_rasterise_fwd_gbuffer"));
+    g_api.fwd_resolve = reinterpret_cast<decltype(g_api.fwd_resolve)>(sym("dirt_rasterise_fwd_resolve"));
     g_api.bwd = reinterpret_cast<decltype(g_api.bwd)>(sym("dirt_rasterise_bwd"));
     g_api.scratch_clear = reinterpret_cast<decltype(g_api.scratch_clear)>(sym("dirt_scratch_clear"));
     g_api.check_faces = reinterpret_cast<decltype(g_api.check_faces)>(sym("dirt_check_faces"));
@@ -167,6 +169,86 @@ struct ScratchCache {
     }
 } g_scratch;
 
+// Renders that share their geometry (samples/deferred.py:63-83 renders one mesh three times, as
+// positions, albedo and normals): the last plain Gouraud forward per (device, stream, capture) remembers its geometry
+// -- the vertices' and faces' storage, offset, sizes, strides and version counters (detached aliases, so no autograd
+// graph is kept) -- with its g-buffer and saved records.  A forward whose vertices and faces are the same tensors
+// (or views of the same storage, same elements), unmodified since (version counters unchanged: every in-place op on
+// them or a view bumps it), at the same B, H, W, F, takes dirt_rasterise_fwd_resolve: no setup, bins or visibility
+// pass, pixels bit-identical.  Its backward reads the shared saved records (read-only) and its own g-buffer copy.
+// Writes that bypass the version counter (`.data`, raw pointers) are not seen -- the same limitation as autograd's
+// own saved-tensor checks; DIRT_SHARE_GEOMETRY=0 turns the cache off.  A capture's entries are its own (its g-buffer
+// is recomputed by its replays), and eager entries are never used inside a capture or the other way round.
+struct GeomCache {
+    struct Entry {
+        int dev = -1;
+        uintptr_t stream = 0;
+        unsigned long long cid = 0;
+        at::Tensor v, f, gbuffer, saved;
+        int64_t vver = 0, fver = 0, H = 0, W = 0;
+    };
+    std::mutex mu;
+    std::list<Entry> entries;  // one per (device, stream, capture id), a few at most
+    static bool enabled()
+    {
+        static int v = -1;
+        if (v < 0) {
+            const char *e = getenv("DIRT_SHARE_GEOMETRY");
+            v = (e && *e) ? (atoi(e) != 0) : 1;
+        }
+        return v != 0;
+    }
+    // the same elements of the same storage (strides of size-1 dimensions do not matter)
+    static bool same(const at::Tensor &a, const at::Tensor &b)
+    {
+        if (!a.defined() || !b.defined() || a.unsafeGetTensorImpl()->storage().unsafeGetStorageImpl() !=
+                                                b.unsafeGetTensorImpl()->storage().unsafeGetStorageImpl() ||
+            a.storage_offset() != b.storage_offset() || a.sizes() != b.sizes() || a.scalar_type() != b.scalar_type())
+            return false;
+        for (int64_t d = 0; d < a.dim(); ++d)
+            if (a.size(d) > 1 && a.stride(d) != b.stride(d)) return false;
+        return true;
+    }
+    // the shared (gbuffer, saved) of an unchanged geometry, or undefined tensors
+    std::pair<at::Tensor, at::Tensor> find(int dev, hipStream_t stream, unsigned long long cid, const at::Tensor &v,
+                                           const at::Tensor &f, int64_t H, int64_t W)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (const Entry &e : entries)
+            if (e.dev == dev && e.stream == reinterpret_cast<uintptr_t>(stream) && e.cid == cid && e.H == H && e.W == W &&
+                same(e.v, v) && same(e.f, f) && e.vver == (int64_t)v._version() && e.fver == (int64_t)f._version())
+                return {e.gbuffer, e.saved};
+        return {at::Tensor(), at::Tensor()};
+    }
+    void store(int dev, hipStream_t stream, unsigned long long cid, const at::Tensor &v, const at::Tensor &f, int64_t H,
+               int64_t W, const at::Tensor &gbuffer, const at::Tensor &saved)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        entries.remove_if([&](const Entry &e) {
+            return e.dev == dev && e.stream == reinterpret_cast<uintptr_t>(stream) && e.cid == cid;
+        });
+        Entry e;
+        e.dev = dev;
+        e.stream = reinterpret_cast<uintptr_t>(stream);
+        e.cid = cid;
+        e.v = v.detach();
+        e.f = f.detach();
+        e.vver = (int64_t)v._version();
+        e.fver = (int64_t)f._version();
+        e.H = H;
+        e.W = W;
+        e.gbuffer = gbuffer;
+        e.saved = saved;
+        entries.push_front(e);
+        while (entries.size() > 8) entries.pop_back();
+    }
+    void clear()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        entries.clear();
+    }
+} g_geom;
+
 using torch::autograd::AutogradContext;
 using torch::autograd::variable_list;
 
@@ -187,7 +269,6 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
         const auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
         at::Tensor pixels = at::empty({B, H, W, C}, f32);
         at::Tensor gbuffer = at::empty({B, H, W}, i32);
-        at::Tensor saved = at::empty({(int64_t)std::max<size_t>(saved_bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
         // (needs_input_grad is only defined when the node records a graph: grad_possible, decided outside
         // forward where GradMode is visible)
         const bool need_grad = grad_possible && shader_id == DIRT_SHADER_GOURAUD && V > 0 &&
@@ -203,6 +284,25 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
             at::Tensor flag = at::empty({256}, at::TensorOptions().dtype(at::kByte).device(dev));
             check(g_api.check_faces(faces.data_ptr<int32_t>(), (int)B, (int)V, (int)F, flag.data_ptr(), 256, stream));
         }
+        // a render of the same geometry as the last plain Gouraud forward on this stream: the resolve alone
+        const bool shareable = GeomCache::enabled() && shader_id == DIRT_SHADER_GOURAUD && !want_gbuf && F > 0 &&
+                               !(fwd_flags & (DIRT_FWD_DEEP_CULL | DIRT_FWD_DEEP_CULL_OFF));
+        const unsigned long long cid = shareable ? ScratchCache::capture_id(stream) : 0ull;
+        if (shareable) {
+            std::pair<at::Tensor, at::Tensor> hit = g_geom.find(dev.index(), stream, cid, vertices, faces, H, W);
+            if (hit.first.defined()) {
+                check(g_api.fwd_resolve(background.data_ptr<float>(), vertex_colors.data_ptr<float>(), (int)B, (int)H,
+                                        (int)W, (int)C, (int)V, (int)F, hit.first.data_ptr<int32_t>(),
+                                        hit.second.data_ptr(), (size_t)hit.second.numel(), pixels.data_ptr<float>(),
+                                        gbuffer.data_ptr<int32_t>(), want_v ? gv.data_ptr<float>() : nullptr,
+                                        want_c ? gc.data_ptr<float>() : nullptr, stream));
+                finish_forward(ctx, vertices, vertex_colors, faces, pixels, gbuffer, hit.second, B, H, W, C, V, F,
+                               shader_id, need_grad, want_v, want_c, gv, gc);
+                ctx->mark_non_differentiable({gbuffer});
+                return {pixels, gbuffer};
+            }
+        }
+        at::Tensor saved = at::empty({(int64_t)std::max<size_t>(saved_bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
         const ScratchCache::Key skey{dev.index(), reinterpret_cast<uintptr_t>(stream), B, H, W, F, bin_capacity};
         at::Tensor scratch = g_scratch.get(skey, scratch_bytes, dev, stream);
         float *zgv = want_v ? gv.data_ptr<float>() : nullptr;
@@ -237,6 +337,20 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
                             (unsigned)fwd_flags | DIRT_FWD_SCRATCH_CLEAN, zgv, zgc, stream));
         }
         drop.armed = false;
+        if (shareable) g_geom.store(dev.index(), stream, cid, vertices, faces, H, W, gbuffer, saved);
+        finish_forward(ctx, vertices, vertex_colors, faces, pixels, gbuffer, saved, B, H, W, C, V, F, shader_id,
+                       need_grad, want_v, want_c, gv, gc);
+        variable_list nd(out.begin() + 1, out.end());
+        ctx->mark_non_differentiable(nd);
+        return out;
+    }
+
+    static void finish_forward(AutogradContext *ctx, const at::Tensor &vertices, const at::Tensor &vertex_colors,
+                               const at::Tensor &faces, const at::Tensor &pixels, const at::Tensor &gbuffer,
+                               const at::Tensor &saved, int64_t B, int64_t H, int64_t W, int64_t C, int64_t V, int64_t F,
+                               int64_t shader_id, bool need_grad, bool want_v, bool want_c, const at::Tensor &gv,
+                               const at::Tensor &gc)
+    {
         // the backward takes the pixels' gradient only: without this, autograd would fill a zero gradient for
         // each non-differentiable output (the int32 g-buffer: a 4 MB fill kernel per backward at config 3)
         ctx->set_materialize_grads(false);
@@ -248,9 +362,6 @@ struct RasteriseFn : public torch::autograd::Function<RasteriseFn> {
             ctx->saved_data["gv"] = gv;
             ctx->saved_data["gc"] = gc;
         }
-        variable_list nd(out.begin() + 1, out.end());
-        ctx->mark_non_differentiable(nd);
-        return out;
     }
 
     static variable_list backward(AutogradContext *ctx, variable_list grads)
@@ -550,7 +661,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
           py::arg("background"), py::arg("vertices"), py::arg("vertex_colors"), py::arg("faces"), py::arg("height"),
           py::arg("width"), py::arg("channels"), py::arg("bin_capacity"), py::arg("want_gbuf"), py::arg("check_faces"),
           py::arg("fwd_flags") = (int64_t)DIRT_FWD_SCRATCH_CLEAN);
-    m.def("scratch_cache_clear", [](bool force) { g_scratch.clear(force); }, py::arg("force") = false);
+    m.def("scratch_cache_clear", [](bool force) {
+        g_scratch.clear(force);
+        g_geom.clear();
+    }, py::arg("force") = false);
     m.def("scratch_cache_size", []() { return g_scratch.size(); });
     // fused lighting helpers: operands already CUDA float32 and contiguous (dirt_amd/lighting.py checks)
     m.def("vertex_normals", [](at::Tensor vertices, at::Tensor faces) {

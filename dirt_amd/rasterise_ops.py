@@ -161,6 +161,51 @@ class _Workspace(_CaptureKeyedCache):
 _workspace = _Workspace()
 
 
+class _GeomCache:
+    """Renders that share their geometry (samples/deferred.py:63-83 renders one mesh three times):
+    the Python twin of _dirt_torch's GeomCache.  The last plain Gouraud forward per (device, stream, capture id)
+    remembers its geometry -- vertices' and faces' storage, offset, shape, strides and version counters, as detached
+    aliases -- with its g-buffer and saved records; a forward on the same, unmodified tensors (or views of the same
+    elements) at the same frame size takes dirt_rasterise_fwd_resolve (the resolve alone, pixels bit-identical).
+    Writes that bypass the version counter (`.data`, raw pointers) are not seen, like autograd's own saved-tensor
+    checks; DIRT_SHARE_GEOMETRY=0 turns it off."""
+
+    enabled = os.environ.get("DIRT_SHARE_GEOMETRY", "1") not in ("", "0")
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._d = collections.OrderedDict()
+
+    @staticmethod
+    def _ident(t):
+        # (strides of size-1 dimensions do not matter)
+        return (t.untyped_storage()._cdata, t.storage_offset(), tuple(t.shape),
+                tuple(s if n > 1 else 0 for s, n in zip(t.stride(), t.shape)), t.dtype, t._version)
+
+    def find(self, key, vertices, faces, H, W):
+        with self._lock:
+            e = self._d.get(key)
+        if e is None or e[0] != (self._ident(vertices), self._ident(faces), H, W):
+            return None
+        return e[2], e[3]
+
+    def store(self, key, vertices, faces, H, W, gbuffer, saved):
+        with self._lock:
+            # (the detached aliases keep the storages alive, so their addresses identify them)
+            self._d[key] = ((self._ident(vertices), self._ident(faces), H, W), (vertices.detach(), faces.detach()),
+                            gbuffer, saved)
+            self._d.move_to_end(key)
+            while len(self._d) > 8:
+                self._d.popitem(last=False)
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+
+
+_geom = _GeomCache()
+
+
 def _check_faces_now(faces, B, V, F, stream):
     """Opt-in range check of the face indices (a kernel and a host sync): raises IndexError like the
     SURVEY 8b return code 2.  The reference reads out of bounds (csrc/rasterise_egl.cpp:309-336 checks
@@ -187,7 +232,6 @@ class _RasteriseFunction(torch.autograd.Function):
         saved_bytes, scratch_bytes = _lib.workspace_sizes(B, H, W, C, V, F, bin_capacity)
         pixels = torch.empty((B, H, W, C), dtype=torch.float32, device=dev)
         gbuffer = torch.empty((B, H, W), dtype=torch.int32, device=dev)
-        saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
         need_grad = shader_id == _lib.SHADER_GOURAUD and any(ctx.needs_input_grad[:3]) and V > 0
         # the accumulators the backward fills (it computes only those; background-only: both)
         want_v, want_c = need_grad and ctx.needs_input_grad[1], need_grad and ctx.needs_input_grad[2]
@@ -199,6 +243,22 @@ class _RasteriseFunction(torch.autograd.Function):
             stream = torch.cuda.current_stream(dev).cuda_stream
             if check_faces:
                 _check_faces_now(faces, B, V, F, stream)
+            shareable = (_GeomCache.enabled and shader_id == _lib.SHADER_GOURAUD and not want_gbuf and F > 0 and
+                         not (_FWD_FLAGS & (_lib.FWD_DEEP_CULL | _lib.FWD_DEEP_CULL_OFF)))
+            gkey = None
+            if shareable:
+                gkey = (dev, stream, _lib.capture_id(stream) if torch.cuda.is_current_stream_capturing() else 0)
+                hit = _geom.find(gkey, vertices, faces, H, W)
+                if hit is not None:
+                    # a render of the geometry the last forward on this stream rendered: the resolve alone
+                    gb_in, saved = hit
+                    _lib.check(lib.dirt_rasterise_fwd_resolve(
+                        background.data_ptr(), vertex_colors.data_ptr(), B, H, W, C, V, F, gb_in.data_ptr(),
+                        saved.data_ptr(), saved.numel(), pixels.data_ptr(), gbuffer.data_ptr(),
+                        gv.data_ptr() if want_v else None, gc.data_ptr() if want_c else None, stream))
+                    return _RasteriseFunction._finish(ctx, vertices, vertex_colors, faces, pixels, gbuffer, saved, (),
+                                                      (B, H, W, C, V, F), shader_id, need_grad, gv, gc, want_v, want_c)
+            saved = torch.empty((max(saved_bytes, 1),), dtype=torch.uint8, device=dev)
             layout = (B, H, W, F, bin_capacity)
             scratch = _workspace.scratch(dev, stream, layout, scratch_bytes)
             cam = camera_pos.data_ptr() if camera_pos is not None else None
@@ -210,8 +270,16 @@ class _RasteriseFunction(torch.autograd.Function):
             except Exception:
                 _workspace.discard(dev, stream, layout)  # its count sets may be dirty now
                 raise
+            if shareable:
+                _geom.store(gkey, vertices, faces, H, W, gbuffer, saved)
+        return _RasteriseFunction._finish(ctx, vertices, vertex_colors, faces, pixels, gbuffer, saved, extra,
+                                          (B, H, W, C, V, F), shader_id, need_grad, gv, gc, want_v, want_c)
+
+    @staticmethod
+    def _finish(ctx, vertices, vertex_colors, faces, pixels, gbuffer, saved, extra, dims, shader_id, need_grad, gv, gc,
+                want_v, want_c):
         ctx.save_for_backward(vertices, vertex_colors, faces, pixels, gbuffer, saved)
-        ctx.dims = (B, H, W, C, V, F)
+        ctx.dims = dims
         ctx.shader_id = shader_id
         ctx.prezeroed = (gv, gc) if need_grad else None
         ctx.want = (want_v, want_c) if need_grad else (True, True)
@@ -363,6 +431,7 @@ def workspace_cache_clear(force=False):
     Scratch made inside a graph capture stays pinned (its graph writes it at every replay) unless `force`: call
     `workspace_cache_clear(force=True)` once the graphs captured through the op are destroyed."""
     _workspace.clear(force)
+    _geom.clear()
     from . import op_library
     op_library._stash_workspaces.clear(force)
     ext = _torch_ext()

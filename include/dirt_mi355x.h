@@ -75,7 +75,8 @@ extern "C" {
  * dirt_bwd_recompute_workspace_size; 9: + the fused lighting helpers dirt_vertex_normals_*,
  * dirt_diffuse_directional_*, dirt_specular_directional_*, dirt_diffuse_point_*; 10: + dirt_stream_capture_id;
  * 11: + dirt_rasterise_fwd_stash, the recompute workspace grows by the gradient stash; 12: the Gouraud forward
- * picks the occluder culling by itself (DIRT_FWD_DEEP_CULL forces it, + DIRT_FWD_DEEP_CULL_OFF)) */
+ * picks the occluder culling by itself (DIRT_FWD_DEEP_CULL forces it, + DIRT_FWD_DEEP_CULL_OFF); 13: +
+ * dirt_rasterise_fwd_resolve) */
 int dirt_abi_version(void);
 
 /* Byte sizes of the caller-provided buffers for one call.
@@ -115,6 +116,19 @@ int dirt_rasterise_fwd_gbuffer(const float *background, const float *vertices, c
                                void *scratch, size_t scratch_bytes, int64_t bin_capacity, unsigned flags,
                                float *zero_grad_vertices, float *zero_grad_vertex_colors,
                                float *depth, float *barycentrics, int32_t *face_ids, void *stream);
+/* Forward of a render that shares its geometry with an earlier one (ABI 13): the same vertices, faces, B, H, W and
+ * default bin capacity as the Gouraud dirt_rasterise_fwd that wrote `gbuffer_in` and `saved`, other vertex colours
+ * [B,V,C] and background [B,H,W,C] (C may differ from that forward's).  Only the resolve runs -- per pixel the visible
+ * record from gbuffer_in, its perspective-correct barycentrics from saved, the Gouraud colour of these vertex colours
+ * or this background -- so the pixels are bit-identical to a dirt_rasterise_fwd of the same inputs, whose coverage
+ * and depth depend on the geometry only.  `gbuffer` [B,H,W] receives this render's copy of the g-buffer (the same
+ * words); gbuffer_in and saved are only read, and the later dirt_rasterise_bwd of this render takes `gbuffer` and the
+ * same `saved`.  zero_grad_*: as dirt_rasterise_fwd (zero-filled in passing).  samples/deferred.py:63-83 renders
+ * one geometry three times (positions, albedo, normals). */
+int dirt_rasterise_fwd_resolve(const float *background, const float *vertex_colors, int B, int H, int W, int C, int V,
+                               int F, const int32_t *gbuffer_in, const void *saved, size_t saved_bytes, float *pixels,
+                               int32_t *gbuffer, float *zero_grad_vertices, float *zero_grad_vertex_colors,
+                               void *stream);
 /* Forward of the Hill op (csrc/hill.cpp:282-498, REGISTER_OP("Hill") :33-53): DIRT_SHADER_HILL with a
  * terrain lookup `terrain` [B,H,W,terrain_channels] (1, 3 or 4 channels, uploaded like a background,
  * rasterise_egl.cu:33-47) in place of the background; vertex colours are not read.  pixels [B,H,W,C];

@@ -49,7 +49,7 @@ def test_header_flags_match_the_binding():
 
 def test_abi_version_and_workspace_sizes():
     lib = _lib.load()
-    assert lib.dirt_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.dirt_abi_version() == _lib.ABI_VERSION == 13
     saved, scratch = _lib.workspace_sizes(1, 1024, 1024, 3, 150000, 50000)
     assert saved >= 50000 * 6 * 128 + 50000 * 32  # 128-B records (6 slots/face) + 32-B face data
     assert scratch > 0
