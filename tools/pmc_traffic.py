@@ -28,7 +28,10 @@ def per_kernel(path, counter):
 
 
 def main():
+    # python tools/pmc_traffic.py SRC DST [TREE]: TREE (the git commit the measured build came from) and the box
+    # this runs on are recorded as `measured_on` (run it on the GPU box, after the passes)
     src, dst = sys.argv[1], sys.argv[2]
+    tree = sys.argv[3] if len(sys.argv) > 3 else None
     cal, _ = per_kernel(src + '/cal/run_counter_collection.csv', 'FETCH_SIZE')
     fetch, meta = per_kernel(src + '/FETCH_SIZE/run_counter_collection.csv', 'FETCH_SIZE')
     write, _ = per_kernel(src + '/WRITE_SIZE/run_counter_collection.csv', 'WRITE_SIZE')
@@ -37,6 +40,14 @@ def main():
     out = {"method": "2 x FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 --pmc, separate passes, bench.py c3 "
                      "eager launches, median over launches)",
            "fetch_calibration": {k: round(f, 4) for k, f in factors.items()}, "kernels": {}}
+    import platform
+    box = {"host": platform.node()}
+    try:
+        import torch
+        box["gpu"] = torch.cuda.get_device_name(0)
+    except Exception:  # noqa: BLE001 -- informative only
+        pass
+    out["measured_on"] = {"tree": tree, **box}
     for k in sorted(set(fetch) | set(write)):
         if 'fillBuffer' in k or 'read_bytes' in k:
             continue
