@@ -158,3 +158,32 @@ def test_fused_lighting_bindings_check_their_operands():
     out = lighting.diffuse_directional(n, torch.ones(5, 3), torch.tensor([0., 0., -1.]), torch.ones(3))
     ref = lighting._diffuse_directional_ops(n, torch.ones(5, 3), torch.tensor([0., 0., -1.]), torch.ones(3), True)
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+def test_shared_geometry_identity_rule():
+    """The public op shares a render's setup and visibility with the previous forward only for the same elements of
+    the same storage, unmodified (torch version counters): views of them match, in-place edits, clones and other
+    layouts do not (rasterise_ops._GeomCache; the C++ op applies the same rule)."""
+    ident = rasterise_ops._GeomCache._ident
+    v = torch.arange(24, dtype=torch.float32).reshape(1, 6, 4)
+    f = torch.arange(6, dtype=torch.int32).reshape(1, 2, 3)
+    base = ident(v)
+    assert ident(v) == base
+    assert ident(v[0][None]) == base  # a view of the same elements (the size-1 dimension's stride is ignored)
+    assert ident(v.view(1, 6, 4)) == base
+    assert ident(v.clone()) != base  # equal values, another storage
+    assert ident(v[:, :5]) != base  # other elements
+    assert ident(v.transpose(1, 2).contiguous().transpose(1, 2)) != base  # another layout
+    v.mul_(1.0)  # in place, same values: the version counter moved
+    assert ident(v) != base
+    c = rasterise_ops._GeomCache()
+    gb, saved = torch.zeros(1), torch.zeros(2)
+    key = ("dev", 0, 0)
+    c.store(key, v, f, 8, 8, gb, saved)
+    assert c.find(key, v, f, 8, 8) == (gb, saved)
+    assert c.find(key, v, f, 8, 9) is None  # other frame size
+    assert c.find(("dev", 1, 0), v, f, 8, 8) is None  # other stream / capture
+    f[0, 0, 0] = 5  # faces edited in place
+    assert c.find(key, v, f, 8, 8) is None
+    c.clear()
+    assert c.find(key, v, f, 8, 8) is None

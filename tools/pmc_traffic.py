@@ -44,7 +44,7 @@ def main():
     box = {"host": platform.node()}
     try:
         import torch
-        box["gpu"] = torch.cuda.get_device_name(0)
+        box["gpu"] = "%s (%s)" % (torch.cuda.get_device_name(0), torch.cuda.get_device_properties(0).gcnArchName)
     except Exception:  # noqa: BLE001 -- informative only
         pass
     out["measured_on"] = {"tree": tree, **box}
