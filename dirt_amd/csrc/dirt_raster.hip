@@ -1114,7 +1114,7 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
         break
     switch (variant) {
         V_GRAD(0); V_GRAD(1); V_GRAD(2); V_GRAD(3); V_GRAD(4); V_GRAD(5); V_GRAD(8); V_GRAD(16); V_GRAD(7);
-        V_GRAD(32); V_GRAD(64); V_GRAD(72); V_GRAD(128); V_GRAD(256); V_GRAD(512);
+        V_GRAD(32); V_GRAD(64); V_GRAD(72); V_GRAD(128); V_GRAD(256);
     default:
         return fail(DIRT_EINVAL, "dirt_debug_bwd_variant: unknown variant");
     }

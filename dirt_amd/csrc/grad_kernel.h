@@ -131,51 +131,28 @@ constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS
 constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
 static_assert(kSlots <= 128, "slot ids (0 .. kSlots-1) are stored as int8");
 
-// LDS-resident copy of the edge part of the records seen in a tile + halo (for coverage tests of a
-// neighbour's face) and of their vertex ids (for the flush).
+// The records visible in a tile (its own pixels; the halo's are not needed: pair coverage comes from the
+// forward's bits): keys for the run-tail ranges of the reduction and vertex ids for the flush.  Each lane reads
+// its own pixel's record itself (phase A, right after its g-buffer word), so nothing else is kept here.
 struct SlotTable {
     int32_t key[kSlots];     // g-buffer word (record index | clipped flag), -1 = free
     int8_t list[kSlots];     // occupied slots in insertion order
-    int32_t A[3][kSlots], B[3][kSlots];
-    int32_t e[3][kSlots];      // small records: E + owned at the halo origin pixel (see kGradSmallEdge)
-    uint32_t bx[kSlots], by[kSlots];  // i0 | i1 << 16 (bit 31: large record, use the global Rec)
     int32_t v[3][kSlots];    // vertex ids, indexed by list position
-    float q[3][kSlots];      // FaceData.q of the record's face: 1/w (non-clipped face), parent clip w
-                             // (clipped face: the record's own 1/w are read from the record)
-    float h2d[kSlots];                  // 1 / (2 D), D = E0 + E1 + E2 (constant over the plane)
     int32_t n;
 };
 
-// A record is "small" for the backward when every |A|, |B| < 2^14 (edges shorter than 64 px).  Such a
-// record is visible somewhere in the 18x18 tile + halo region, so at every region pixel its edge values
-// satisfy |E| < 2^28 (E at a covered pixel) + 2 * 2^14 * 33 * 256 < 2^30: exact in int32, and a
-// coverage test is E0 + A*256*hx + B*256*hy with 24-bit multiplies (hx in 0..33, hy in 0..17).
+// A record is "small" when every |A|, |B| < 2^14 (edges shorter than 64 px): at a pixel it covers, every
+// offset to its vertex 0 is below 2^14 sub-pixels, so E = A dx + B dy (+ D) is exact in int32 with 24-bit
+// multiplies (|E| < 2^30), as in the raster's resolve; larger records take the int64 edge values.
 constexpr int32_t kGradSmallEdge = 1 << 14;
-constexpr uint32_t kSlotLarge = 0x80000000u;
-
-__device__ __forceinline__ bool slot_is_large(const SlotTable &T, int s) { return (T.bx[s] & kSlotLarge) != 0; }
-
-// exact coverage of region pixel (hx, hy) = absolute (i, j) by small slot s (bbox + R2/R3 edge test)
-__device__ __forceinline__ bool slot_covers_small(const SlotTable &T, int s, int hx, int hy, int i, int j)
-{
-    const uint32_t bx = T.bx[s], by = T.by[s];
-    if (i < (int)(bx & 0xffff) || i > (int)((bx >> 16) & 0x7fff) || j < (int)(by & 0xffff) || j > (int)(by >> 16))
-        return false;
-    const int32_t x = hx * 256, y = hy * 256;
-    const int32_t e0 = T.e[0][s] + __mul24(T.A[0][s], x) + __mul24(T.B[0][s], y);
-    const int32_t e1 = T.e[1][s] + __mul24(T.A[1][s], x) + __mul24(T.B[1][s], y);
-    const int32_t e2 = T.e[2][s] + __mul24(T.A[2][s], x) + __mul24(T.B[2][s], y);
-    return min(e0, min(e1, e2)) > 0;
-}
-
-__device__ __forceinline__ int32_t owned_bit(int32_t A, int32_t B) { return (A > 0 || (A == 0 && B < 0)) ? 1 : 0; }
 
 __device__ __forceinline__ int slot_hash(int32_t key) { return (int)(((uint32_t)key * 2654435761u) >> 25) & (kSlots - 1); }
 
 // Insert `key` for every lane with `want` (called by the whole wave, converged): probes advance in
 // lockstep, and the lanes that created a slot append it to the slot list with one atomic per wave.
-// Returns the slot, kNoSlot if the table is full, -1 where !want.
-__device__ __forceinline__ int slot_insert_wave(SlotTable &T, int32_t key, bool want)
+// Returns the slot, kNoSlot if the table is full, -1 where !want; a lane that created its slot gets the slot's
+// list position in *list_pos (others: unchanged).
+__device__ __forceinline__ int slot_insert_wave(SlotTable &T, int32_t key, bool want, int *list_pos)
 {
     int slot = slot_hash(key);
     int result = want ? kNoSlot : -1;
@@ -198,9 +175,12 @@ __device__ __forceinline__ int slot_insert_wave(SlotTable &T, int32_t key, bool 
         int base = 0;
         if ((threadIdx.x & 63) == 0) base = atomicAdd(&T.n, __popcll(mask));
         base = __shfl(base, 0, 64);
-        if (fresh)
-            T.list[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = (int8_t)result;
+        const int p = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (fresh) {
+            T.list[p] = (int8_t)result;
+            *list_pos = p;
+        }
     }
     return result;
 }
@@ -319,7 +299,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     constexpr bool kPacked = CM == 3;
     __shared__ int32_t s_gb[kPacked ? 1 : kHaloPix];
     __shared__ uint8_t s_cov[kPacked ? 1 : kHaloPix];  // neighbour_coverage() bits of the pixel's face (forward)
-    __shared__ int8_t s_slot[kHaloPix];  // slot of the pixel's record, -1 none, kNoSlot table full
 #ifndef DIRT_GRAD_PAIR_RECOMPUTE
 #define DIRT_GRAD_PAIR_RECOMPUTE 1
 #endif
@@ -394,6 +373,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     // the staged pixels' g-buffer words and G / I (for the staged pair scalars below, !kRecompute)
     int32_t gbv[2];
     float Gv[2][CM], Iv[2][CM];
+    // The lane's own pixel: its g-buffer word (loaded with the staging loads) and its record's edge part and FaceData,
+    // read by the lane itself right after the staging round trip -- in flight across the LDS stores, the first barrier
+    // and the slot inserts, instead of a second round trip after them by the slot table's fill (phase B is the first
+    // reader; the records of a wave's pixels are a handful, so the loads are mostly L1 hits).
+    int32_t g_own = -2;
+    EdgePart me{};
+    FaceData mfd{};
     {
         // every load of both passes in flight before the first LDS store (kHaloPix <= 2 * NT)
         static_assert(kHaloPix <= 2 * NT, "two staging passes");
@@ -404,6 +390,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
         const float *gp_f = grad_pixels + fpix * C, *px_f = pixels + fpix * C;
         uint32_t cvv[2];
         bool ok[2];
+        if (in_frame) g_own = gb_f[(uint32_t)((H - 1 - j) * W + i)];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int k = t + NT * u;
@@ -475,30 +462,48 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
                     }
             }
         }
+        // (after the stores: issued before them, the loads would make the stores' wait cover them too)
+        if (g_own >= 0) {
+            const int32_t ri = g_own & kGbufIndexMask;
+            me = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
+            mfd = fdata_frame[face_of_record(ri, F)];
+        }
     }
     __syncthreads();
     PHASE_TS(1);
     const int prow = (ly + 1) & 1;  // parity of this pixel's region row (packed layout)
     const int32_t gp = in_frame ? ld_gb(kme, prow) : -2;
+    int sp, fpos = -1;  // the own pixel's slot; the list position of a slot this lane created
     {
-        // the tile's own records (run heads only; all distinct keys may not fit: the rest read global
-        // memory).  The halo's records are not needed: pair coverage comes from the forward's bits.
+        // the tile's records (run heads only; all distinct keys may not fit: the rest go to global memory)
         const int32_t g = ld_gb(kme, prow);
         const int key = g >= 0 ? g : -1;
         const int start = run_start(key, lr);
-        // (AB & 512, ablation: the slot table handed over instead of built -- slots from the key, no CAS inserts;
-        // timing only, wrong gradients)
-        int slot = (AB & 512) ? (key >= 0 && start == lr ? (key & 31) : -1) : slot_insert_wave(T, key, key >= 0 && start == lr);
+        int slot = slot_insert_wave(T, key, key >= 0 && start == lr, &fpos);
         if (key >= 0 && start == lr && slot >= 0) atomicAdd(&s_tcnt[slot], 1);  // one run (one tail later)
         slot = __shfl(slot, (t & 48) + start, 64);
-        s_slot[kme] = key >= 0 ? slot : -1;
+        sp = key >= 0 ? slot : -1;
+    }
+    if constexpr (!kRecompute) {
+        // staged pair scalars: the lane that staged region pixel k computes the pairs starting there that phase B
+        // reads -- (k, k+x) for hx in 0..TWX, hy in 1..16 and (k, k+y) for hx in 1..TWX, hy in 0..16 -- with k's own
+        // G / I still in its registers (only the neighbour's come from LDS)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = t + NT * u;
+            if (k >= kHaloPix) continue;
+            const int hx = k % kHalo, hy = k / kHalo;
+            const bool need_x = hx <= TWX && hy >= 1 && hy <= TH;
+            const bool need_y = hx >= 1 && hx <= TWX && hy <= TH;
+            if (need_x) s_sx[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + 1, C);
+            if (need_y) s_sy[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + kHalo, C);
+        }
     }
     __syncthreads();
     PHASE_TS(2);
     PHASE_TS(3);
-    const int nslots = (AB & 512) ? 32 : T.n;
+    const int nslots = T.n;
     static_assert(kSlots <= 64, "one slot per lane of wave 0");
-    if ((AB & 512) && t < 32) T.list[t] = (int8_t)t;
     if (t < 64) {
         // wave 0: each slot's range of run-tail partials, in slot-list order (exclusive prefix)
         const int sl = t < nslots ? T.list[t] : 0;
@@ -515,63 +520,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
             s_lcnt[t] = cnt;
         }
     }
-    {
-        // slot fill: the record loads are issued first and land while the pair scalars are computed
-        const bool filler = t < nslots;
-        int sf = 0;
-        EdgePart ep{};
-        FaceData fd{};
-        float riw0 = 0.f, riw1 = 0.f, riw2 = 0.f;
-        if (filler && (AB & 512)) {
-            // (ablation: no record / FaceData round trip; made-up small edges and spread vertex ids)
-            sf = t;
-            for (int k = 0; k < 3; ++k) { ep.A[k] = 100 + k; ep.B[k] = -50 + k; fd.v[k] = (int)(((unsigned)blockIdx.x * 96u + 3u * t + k) % (unsigned)max(V, 1)); fd.q[k] = 1.0f; }
-            ep.D = 5000; ep.i0 = 0; ep.i1 = 1000; ep.j0 = 0; ep.j1 = 1000; ep.X0 = 0; ep.Y0 = 0;
-        } else if (filler) {
-            sf = T.list[t];
-            const int32_t ri = T.key[sf] & kGbufIndexMask;
-            ep = *reinterpret_cast<const EdgePart *>(&frame_recs[ri]);
-            fd = fdata_frame[face_of_record(ri, F)];
-            // 1/w of a non-clipped face: its FaceData's q (a clipped record's own 1/w, in the record's second
-            // half, are read in phase B by the lanes that show it)
-            riw0 = fd.q[0]; riw1 = fd.q[1]; riw2 = fd.q[2];
-        }
-        // pair scalars of the pairs starting at an own pixel (right, up) and at the left column /
-        // bottom row of the halo (their one pair into the tile); nothing reads the others
-        if constexpr (!kRecompute) {
-            // staged pair scalars: the lane that staged region pixel k computes the pairs starting there that
-            // phase B reads -- (k, k+x) for hx in 0..TWX, hy in 1..16 and (k, k+y) for hx in 1..TWX, hy in 0..16
-            // -- with k's own G / I still in its registers (only the neighbour's come from LDS)
+    // a slot's creator (a run head showing its record) holds the record's FaceData: its vertex ids for the flush
+    // (read after the barriers of phase C)
+    if (fpos >= 0) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int k = t + NT * u;
-                if (k >= kHaloPix) continue;
-                const int hx = k % kHalo, hy = k / kHalo;
-                const bool need_x = hx <= TWX && hy >= 1 && hy <= TH;
-                const bool need_y = hx >= 1 && hx <= TWX && hy <= TH;
-                if (need_x) s_sx[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + 1, C);
-                if (need_y) s_sy[k] = pair_scalar_own<CP, CM>(gbv[u], Gv[u], Iv[u], s_gb, s_G, s_I, k + kHalo, C);
-            }
-        }
-        if (filler) {
-            bool small = true;
-            int64_t E0[3];
-            edge_values(ep, hi0, hj0, E0);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                T.A[k][sf] = ep.A[k]; T.B[k][sf] = ep.B[k];
-                T.v[k][t] = fd.v[k];  // by list position (read only by the flush)
-                small = small && ep.A[k] > -kGradSmallEdge && ep.A[k] < kGradSmallEdge && ep.B[k] > -kGradSmallEdge &&
-                        ep.B[k] < kGradSmallEdge;
-                T.e[k][sf] = (int32_t)E0[k] + owned_bit(ep.A[k], ep.B[k]);  // meaningful only when small
-            }
-            T.q[0][sf] = riw0; T.q[1][sf] = riw1; T.q[2][sf] = riw2;
-            T.h2d[sf] = 0.5f / (float)ep.D;  // (E_0 + E_1 + E_2 = D at every pixel)
-            T.bx[sf] = (uint32_t)ep.i0 | ((uint32_t)ep.i1 << 16) | (small ? 0u : kSlotLarge);
-            T.by[sf] = (uint32_t)ep.j0 | ((uint32_t)ep.j1 << 16);
-        }
+        for (int k = 0; k < 3; ++k) T.v[k][fpos] = mfd.v[k];
     }
-    __syncthreads();
     PHASE_TS(4);
 
     // ---- phase B: per-pixel contributions to the face visible at this pixel
@@ -592,65 +546,47 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
     float acc[NVM];
 #pragma unroll
     for (int v = 0; v < NVM; ++v) acc[v] = 0.0f;
-    const int sp = rp >= 0 ? s_slot[kme] : -1;
     if (rp >= 0) {
         // Ownership decisions (coverage tests) are exact int64; the interpolation weights use fast
         // reciprocals (contributions agree with the oracle to ~1e-6 relative, far inside the 1e-4
-        // tolerance the atomic summation order already needs).  The own record comes through the
-        // vector-memory path (L1-resident: a wave touches a handful of records).
+        // tolerance the atomic summation order already needs).  The own record's edge part and FaceData
+        // were read in phase A (me, mfd).
         const int f = face_of_record(rp, F);
         const bool multi = (gp & kGbufMulti) != 0;
-        // the own record (large records and the basis of clipped faces): its address is recomputed at
-        // each use from rp (the asm hides the common subexpression) instead of living in two registers
+        // the whole own record (the 1/w and basis of clipped faces): its address is recomputed at each use
+        // from rp (the asm hides the common subexpression) instead of living in two registers
         auto rec = [&]() -> const Rec & {
             int r2 = rp;
             asm volatile("" : "+v"(r2));
             return frame_recs[r2];
         };
-        const int hx = lx + 1, hy = ly + 1;  // region coordinates of this pixel
-        int32_t mA[3], mB[3], eme[3];       // eme: E + owned here (small records only)
-        float iw0, iw1, iw2, h2d;
+        int32_t mA[3], mB[3];
+        float iw0 = mfd.q[0], iw1 = mfd.q[1], iw2 = mfd.q[2];  // 1/w of a non-clipped face
         float fEp[3];
-        bool me_small;
-        if (sp >= 0) {
+        bool small = true;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) { mA[k] = T.A[k][sp]; mB[k] = T.B[k][sp]; }
-            iw0 = T.q[0][sp]; iw1 = T.q[1][sp]; iw2 = T.q[2][sp];  // (1/w unless clipped)
-            h2d = T.h2d[sp];
-            me_small = !slot_is_large(T, sp);
-            if (__builtin_amdgcn_ballot_w64(multi) != 0 && multi) {
-                const Rec &rr = rec();
-                iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
-            }
-        } else {
-            const Rec &rr = rec();
-            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rr);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { mA[k] = me.A[k]; mB[k] = me.B[k]; }
-            if (multi) {
-                iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
-            } else {
-                const FaceData &fq = fdata_frame[f];
-                iw0 = fq.q[0]; iw1 = fq.q[1]; iw2 = fq.q[2];
-            }
-            h2d = 0.5f / (float)me.D;
-            me_small = false;
+        for (int k = 0; k < 3; ++k) {
+            mA[k] = me.A[k];
+            mB[k] = me.B[k];
+            small = small && mA[k] > -kGradSmallEdge && mA[k] < kGradSmallEdge && mB[k] > -kGradSmallEdge &&
+                    mB[k] < kGradSmallEdge;
         }
-        if (me_small) {
+        if (__builtin_amdgcn_ballot_w64(multi) != 0 && multi) {
+            const Rec &rr = rec();
+            iw0 = rr.iw[0]; iw1 = rr.iw[1]; iw2 = rr.iw[2];
+        }
+        const float h2d = 0.5f / (float)me.D;  // 1 / (2 D), D = E0 + E1 + E2 (constant over the plane)
+        if (small) {
+            // E at this pixel (which the record covers): exact in int32, as the raster's resolve
+            const int32_t dx = i * 256 + 128 - me.X0, dy = j * 256 + 128 - me.Y0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                eme[k] = T.e[k][sp] + __mul24(mA[k], hx * 256) + __mul24(mB[k], hy * 256);
-                fEp[k] = (float)(eme[k] - owned_bit(mA[k], mB[k]));
-            }
+            for (int k = 0; k < 3; ++k)
+                fEp[k] = (float)(__mul24(mA[k], dx) + __mul24(mB[k], dy) + (k == 0 ? (int32_t)me.D : 0));
         } else {
-            const EdgePart me = *reinterpret_cast<const EdgePart *>(&rec());
             int64_t Ep[3];
             edge_values(me, i, j, Ep);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                fEp[k] = fast_i64_to_f32(Ep[k]);
-                eme[k] = 0;
-            }
+            for (int k = 0; k < 3; ++k) fEp[k] = fast_i64_to_f32(Ep[k]);
         }
         // the four pairs around the pixel: dir 0 right, 1 left (x axis); 2 up, 3 down (y axis, window).
         // Pass 1 decides ownership (exact integer coverage tests) into 2-bit codes (0 skip, 1 half,
