@@ -18,7 +18,7 @@ from dirt_amd.session import RasteriseSession  # noqa: E402
 
 NAMES = {0: "full", 1: "no pairs", 2: "no colour", 3: "no pairs+colour", 4: "no reduction", 5: "no pairs+reduction",
          7: "nothing but staging", 8: "no flush", 16: "no coverage tests", 32: "no DPP scan (all lanes add)",
-         64: "no LDS adds", 72: "no LDS adds, no flush", 256: "flush without global atomics",
+         64: "no LDS adds", 72: "no LDS adds, no flush", 256: "flush without global atomics"}
 
 
 def main():
