@@ -803,8 +803,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
             for (int v = 0; v < NVM; ++v)
                 if (v < NV) s_part[q * NVM + v] = acc[v];
         } else {
-            const FaceData &fd = fdata_frame[face_of_record(rp, F)];
-            const int32_t vid[3] = {fd.v[0], fd.v[1], fd.v[2]};  // before the atomics (may alias for the compiler)
+            const int32_t vid[3] = {mfd.v[0], mfd.v[1], mfd.v[2]};  // (the lane's own record's face, phase A)
 #pragma unroll
             for (int v = 0; v < NVM; ++v) {
                 if (v >= NV || acc[v] == 0.0f) continue;
