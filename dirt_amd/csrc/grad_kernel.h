@@ -508,12 +508,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, GradGeom<TWX, TH>::NT),
         // wave 0: each slot's range of run-tail partials, in slot-list order (exclusive prefix)
         const int sl = t < nslots ? T.list[t] : 0;
         const int cnt = t < nslots ? s_tcnt[sl] : 0;
+        // inclusive scan over the wave with DPP (no LDS round trips on wave 0's way into phase B): within each
+        // 16-lane row by row_shr 1, 2, 4, 8, then across rows by row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3)
         int inc = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(inc, d, 64);
-            inc += t >= d ? v : 0;
-        }
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xA, 0xF, false);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xC, 0xF, false);
         if (t < nslots) {
             s_toff[sl] = inc - cnt;
             s_lbeg[t] = inc - cnt;
