@@ -385,6 +385,16 @@ def main():
 
     def api_leg():
         import dirt_amd
+        from dirt_amd import rasterise_ops
+        # every step a full forward, as in training (the optimizer changes the vertices each step): the shared-geometry
+        # cache off, which would otherwise serve this leg's repeated, unmodified geometry from its first render
+        share_prev = rasterise_ops.set_geometry_sharing(False)
+        try:
+            api_leg_measure(dirt_amd, rasterise_ops)
+        finally:
+            rasterise_ops.set_geometry_sharing(share_prev)
+
+    def api_leg_measure(dirt_amd, rasterise_ops):
         bg_r, v_r, c_r = (t.clone().requires_grad_(True) for t in (bg, v, c))
 
         def api_step():
@@ -413,9 +423,15 @@ def main():
         n20 = max(2, n_api // 20)
         t_graph20 = timed(g_api20.replay, n20, barrier, world, device, shared)
         del g_api20
+        # for reference: the same eager loop with the cache on (an inference-like repeat of one geometry: every
+        # forward after the first runs the resolve alone); not a training step
+        rasterise_ops.set_geometry_sharing(True)
+        t_sh = sum(timed(api_step, chunk, barrier, world, device, shared) for _ in range(n_chunks))
+        rasterise_ops.set_geometry_sharing(False)
         legs["api_autograd"] = {
             "what": "dirt_amd.rasterise_batch(...) + torch.autograd.grad per step (reference surface "
-                    "dirt/rasterise_ops.py:57-88), fresh outputs per call, cached scratch",
+                    "dirt/rasterise_ops.py:57-88), fresh outputs per call, cached scratch, every forward a full one "
+                    "(shared-geometry cache off; eager_shared_geometry_mpix_s: the same loop with it on)",
             "eager_mpix_s": round(world * B * H * W * n_api / t_eager / 1e6, 1),
             "eager_ms_per_step": round(t_eager * 1e3 / n_api, 4),
             "eager_steps": n_api,
@@ -425,6 +441,8 @@ def main():
             "graph_ms_per_step": round(t_graph * 1e3 / n_api, 4),
             "graph20_mpix_s": round(world * B * H * W * n20 * 20 / t_graph20 / 1e6, 1),
             "graph20_ms_per_step": round(t_graph20 * 1e3 / (n20 * 20), 4),
+            "geometry_sharing": False,
+            "eager_shared_geometry_mpix_s": round(world * B * H * W * n_api / t_sh / 1e6, 1),
             "impl": "C++ autograd function (_dirt_torch)" if dirt_amd.rasterise_ops._torch_ext() is not None
                     else "Python torch.autograd.Function"}
 

@@ -15,6 +15,8 @@
 
 #include <dlfcn.h>
 
+#include <atomic>
+
 #include <list>
 #include <map>
 #include <mutex>
@@ -189,15 +191,16 @@ struct GeomCache {
     };
     std::mutex mu;
     std::list<Entry> entries;  // one per (device, stream, capture id), a few at most
-    static bool enabled()
+    // on unless DIRT_SHARE_GEOMETRY=0; set_geometry_sharing() switches it at run time (both implementations)
+    static std::atomic<int> &flag()
     {
-        static int v = -1;
-        if (v < 0) {
+        static std::atomic<int> v{[] {
             const char *e = getenv("DIRT_SHARE_GEOMETRY");
-            v = (e && *e) ? (atoi(e) != 0) : 1;
-        }
-        return v != 0;
+            return (e && *e) ? (atoi(e) != 0 ? 1 : 0) : 1;
+        }()};
+        return v;
     }
+    static bool enabled() { return flag().load(std::memory_order_relaxed) != 0; }
     // the same elements of the same storage (strides of size-1 dimensions do not matter)
     static bool same(const at::Tensor &a, const at::Tensor &b)
     {
@@ -666,6 +669,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
         g_geom.clear();
     }, py::arg("force") = false);
     m.def("scratch_cache_size", []() { return g_scratch.size(); });
+    m.def("set_geometry_sharing", [](bool on) {
+        const bool prev = GeomCache::flag().exchange(on ? 1 : 0) != 0;
+        if (!on) g_geom.clear();
+        return prev;
+    }, py::arg("enabled"));
     // fused lighting helpers: operands already CUDA float32 and contiguous (dirt_amd/lighting.py checks)
     m.def("vertex_normals", [](at::Tensor vertices, at::Tensor faces) {
         need_api();

@@ -206,6 +206,21 @@ class _GeomCache:
 _geom = _GeomCache()
 
 
+def set_geometry_sharing(enabled):
+    """Turn the shared-geometry cache (renders of one unmodified geometry after the first run the resolve alone) on or
+    off for both implementations of the op; returns the previous setting.  Off: every forward is a full one, as in a
+    training loop whose optimizer changes the vertices each step (tools and benchmarks that repeat one geometry use
+    this to time full steps).  The environment variable DIRT_SHARE_GEOMETRY=0 sets the initial state."""
+    prev = _GeomCache.enabled
+    _GeomCache.enabled = bool(enabled)
+    if not enabled:
+        _geom.clear()
+    ext = _torch_ext()
+    if ext is not None:
+        ext.set_geometry_sharing(bool(enabled))
+    return prev
+
+
 def _check_faces_now(faces, B, V, F, stream):
     """Opt-in range check of the face indices (a kernel and a host sync): raises IndexError like the
     SURVEY 8b return code 2.  The reference reads out of bounds (csrc/rasterise_egl.cpp:309-336 checks

@@ -187,3 +187,16 @@ def test_shared_geometry_identity_rule():
     assert c.find(key, v, f, 8, 8) is None
     c.clear()
     assert c.find(key, v, f, 8, 8) is None
+
+
+def test_geometry_sharing_switch_cpu():
+    """set_geometry_sharing returns the previous setting and drives the cache's switch (no extension on CPU)."""
+    from dirt_amd import rasterise_ops
+    prev = rasterise_ops.set_geometry_sharing(False)
+    try:
+        assert rasterise_ops._GeomCache.enabled is False
+        assert rasterise_ops.set_geometry_sharing(True) is False
+        assert rasterise_ops._GeomCache.enabled is True
+    finally:
+        rasterise_ops.set_geometry_sharing(prev)
+

@@ -159,3 +159,32 @@ def test_shared_geometry_in_a_captured_graph(impl):
         assert_close_grad(out["gv"].cpu().numpy(), gv_total, "grad_vertices replay %d" % rep)
     del graph
     rasterise_ops.workspace_cache_clear(force=True)
+
+
+@pytest.mark.parametrize("impl", ["ext", "py"])
+def test_geometry_sharing_switch(impl):
+    """set_geometry_sharing(False): every render of one geometry is a full one (a training loop's setting, and
+    bench.py's api leg); switched back on, the second render shares again; results are the oracle's either way."""
+    from dirt_amd import rasterise_ops
+    rasterise_ops.workspace_cache_clear(force=True)
+    op = _op(impl)
+    bgs, v, cols, f, (H, W, C) = _scene()
+    vt, ft = _gpu(v), _gpu(f)
+    ct, bt = _gpu(cols[1]), _gpu(bgs[1])
+    ref, _, _ = oracle.rasterise_fwd(bgs[1], v, cols[1], f)
+    prev = rasterise_ops.set_geometry_sharing(False)
+    try:
+        for _ in range(3):
+            px, n = _setup_launches(lambda: op(bt, vt, ct, ft, H, W, C))
+            assert n == 1
+            np.testing.assert_array_equal(px.cpu().numpy(), ref)
+        assert rasterise_ops.set_geometry_sharing(True) is False
+        counts = []
+        for _ in range(2):
+            px, n = _setup_launches(lambda: op(bt, vt, ct, ft, H, W, C))
+            counts.append(n)
+            np.testing.assert_array_equal(px.cpu().numpy(), ref)
+        assert counts == [1, 0]
+    finally:
+        rasterise_ops.set_geometry_sharing(prev)
+
