@@ -1,6 +1,6 @@
 """FETCH_SIZE calibration on gfx950: read 256 MiB once with 4-, 12- and 16-byte lane accesses
 (dirt_debug_read_bytes) so that rocprofv3 FETCH_SIZE (KB) can be converted to bytes per access width.
-Run under rocprofv3 --pmc FETCH_SIZE (tools/gpu_pmc.sh does); the buffer exceeds the 256 MiB
+Run under rocprofv3 --pmc FETCH_SIZE (tools/gpu_final.sh and tools/gpu_traffic.sh do); the buffer exceeds the 256 MiB
 Infinity Cache together with the flush buffer, so the reads come from HBM."""
 import ctypes
 import os
