@@ -127,7 +127,7 @@ struct GradGeom {
     static constexpr int HY = TH + 2;
     static constexpr int PIX = HX * HY;
 };
-constexpr int kSlots = 64;         // distinct records per tile+halo kept in LDS (typ. 10-40)
+constexpr int kSlots = 64;         // distinct records of a tile kept in LDS (typ. 10-40)
 constexpr int kNoSlot = -3;        // record not in the slot table: read it from global memory
 static_assert(kSlots <= 128, "slot ids (0 .. kSlots-1) are stored as int8");
 
