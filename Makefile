@@ -20,7 +20,9 @@ WAVEPRIO ?= -mllvm -amdgpu-set-wave-priority
 # 28.44-28.70 Gpixels/s (bench_configs, 10-step graphs).  `make SLP=` builds with it.
 SLP ?= -fno-slp-vectorize
 # SCHED: extra scheduler options for A/B builds (`make variant NAME=x SCHED=...`).  -amdgpu-use-amdgpu-trackers
-# measured within noise over two calls (profiles/r04/ab_sched/), so the product builds without any.
+# measured within noise in round 4 (profiles/r04/ab_sched/) and again in round 6 (+0.3 % over six paired rounds in
+# two calls, -0.5 % in a third; profiles/r06/ab_sched_trackers/); the max-ILP strategy spilled the raster and lost
+# 7 %.  The product builds without any.
 SCHED ?=
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
            -fhip-fp32-correctly-rounded-divide-sqrt $(WAVEPRIO) $(SLP) $(SCHED) -Wall -Wno-unused-function \
