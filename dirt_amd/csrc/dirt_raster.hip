@@ -25,6 +25,7 @@
 // three kernels live in the headers named above, included into this one translation unit.
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <stdint.h>
 #include <stdlib.h>
@@ -1125,6 +1126,51 @@ int dirt_debug_bwd_variant(int variant, const float *pixels, const float *grad_p
     HIP_TRY(hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    return DIRT_OK;
+}
+
+// Debug (synchronises `stream`): the product backward kernel (C == 3, vertex and colour gradients) launched `reps`
+// times through hipExtLaunchKernel with start / stop events, which the runtime takes from the dispatch itself: the mean
+// kernel duration in ms, as rocprofv3 --kernel-trace reports it (an event pair around an ordinary launch, or a graph of
+// back-to-back launches, adds each launch's dependent-launch gap).  Accumulates into the gradient buffers.  bench.py's
+// roofline uses it.  Not part of include/dirt_mi355x.h.
+int dirt_debug_bwd_dispatch_ms(const float *pixels, const float *grad_pixels, const int32_t *gbuffer, const void *saved,
+                               int B, int H, int W, int C, int V, int F, float *grad_vertices, float *grad_vertex_colors,
+                               float *grad_background, int reps, void *stream_, float *ms)
+{
+    if (C != 3 || !grad_vertices || !grad_vertex_colors || reps < 1 || !ms)
+        return fail(DIRT_EINVAL, "dirt_debug_bwd_dispatch_ms: C == 3, both gradient buffers, reps >= 1");
+    int rc = validate(B, H, W, C, V, F);
+    if (rc) return rc;
+    if (!pixels || !grad_pixels || !gbuffer || !saved) return fail(DIRT_EINVAL, "dirt_debug_bwd_dispatch_ms: null pointer");
+    Layout L;
+    rc = make_layout(B, H, W, F, 0, L);
+    if (rc) return rc;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const char *sv = static_cast<const char *>(saved);
+    const Rec *recs = reinterpret_cast<const Rec *>(sv + L.saved_recs);
+    const FaceData *fdata = reinterpret_cast<const FaceData *>(sv + L.saved_fdata);
+    const uint8_t *covbits = reinterpret_cast<const uint8_t *>(sv + L.saved_cov);
+    const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(3) - 1) / grad_tile_h(3);
+    const dim3 grid((unsigned)(gntx * gnty), (unsigned)B), blk(GradGeom<kGradTileW, grad_tile_h(3)>::NT);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    float total = 0.0f;
+    for (int r = 0; r < reps; ++r) {
+        hipExtLaunchKernelGGL(grad_kernel<3, 0, kGradTileW, grad_tile_h(3), 3>, grid, blk, 0u, stream, e0, e1, 0u,
+                              pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx),
+                              L.nrec, grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H),
+                              static_cast<uint32_t *>(nullptr));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventSynchronize(e1));
+        float t = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+        total += t;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *ms = total / (float)reps;
     return DIRT_OK;
 }
 

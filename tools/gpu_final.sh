@@ -18,7 +18,9 @@ for f in ('$O/bench_driver.json','$O/bench.json'):
     d=json.load(open(f)); r=d['roofline']; l=d['legs']
     print(f.split('/')[-1], d['value'], d['ms_per_step'], 'frac', r['frac'], 'avg_us', r['avg_us'], 'ev', r['avg_us_events'], d['kernels_us'], 'api', l.get('api_autograd',{}).get('eager_mpix_s'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --rotate 0 --no-api-leg --no-recompute-leg > $O/bench_prof.json 2> $O/bench_prof.err || { echo "rocprof rc=$?"; tail -5 $O/bench_prof.err; exit 1; }
+# (the driver's command under rocprofv3; tools/trace_summary.py then takes the single-frame launches out of the trace)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 > $O/bench_prof.json 2> $O/bench_prof.err || { echo "rocprof rc=$?"; tail -5 $O/bench_prof.err; exit 1; }
+python3 $R/tools/trace_summary.py $O/prof/run_kernel_trace.csv $O/bench_driver.json > $O/trace_summary.txt && cat $O/trace_summary.txt
 T=$O/traffic
 mkdir -p $T
 timeout -k 10 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $T/cal -o run --output-format csv -- python3 $R/tools/pmc_calibrate.py > $T/cal.log 2>&1 || { echo "calibration rc=$?"; tail -5 $T/cal.log; exit 1; }
