@@ -1153,23 +1153,25 @@ int dirt_debug_bwd_dispatch_ms(const float *pixels, const float *grad_pixels, co
     const uint8_t *covbits = reinterpret_cast<const uint8_t *>(sv + L.saved_cov);
     const int gntx = (W + kGradTileW - 1) / kGradTileW, gnty = (H + grad_tile_h(3) - 1) / grad_tile_h(3);
     const dim3 grid((unsigned)(gntx * gnty), (unsigned)B), blk(GradGeom<kGradTileW, grad_tile_h(3)>::NT);
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t err = hipEventCreate(&e0);
+    if (err == hipSuccess) err = hipEventCreate(&e1);
     float total = 0.0f;
-    for (int r = 0; r < reps; ++r) {
+    for (int r = 0; r < reps && err == hipSuccess; ++r) {
         hipExtLaunchKernelGGL(grad_kernel<3, 0, kGradTileW, grad_tile_h(3), 3>, grid, blk, 0u, stream, e0, e1, 0u,
                               pixels, grad_pixels, gbuffer, covbits, recs, fdata, B, H, W, C, V, F, tile_grid(gntx),
                               L.nrec, grad_vertices, grad_vertex_colors, grad_background, ndc_scale(W, H),
                               static_cast<uint32_t *>(nullptr));
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventSynchronize(e1));
+        err = hipGetLastError();
+        if (err == hipSuccess) err = hipEventSynchronize(e1);
         float t = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+        if (err == hipSuccess) err = hipEventElapsedTime(&t, e0, e1);
         total += t;
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    // (the events are released on every path)
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    HIP_TRY(err);
     *ms = total / (float)reps;
     return DIRT_OK;
 }
